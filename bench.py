@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""Benchmark of the radiance loop: Mrays/s and ms/frame at 1920x1080, 8 spp, 8 bounces on the
+Cornell + OBJ-mesh scene (BASELINE.json `metric`), on 1 GPU or tiled across N GPUs of one node.
+
+A step is one frame: 8 passes (one persistent HIP launch each) over the 1920x1080 frame and the
+8-bit gamma output; with N > 1 each rank renders its interleaved 8-row bands and the float
+accumulation buffer is summed to rank 0 with one RCCL reduce (torch.distributed "nccl"), after
+which rank 0 writes the 8-bit image. Mrays/s = ray segments traced (the live-ray counts the
+reference's thread_shrink returns, summed over passes and depths and over ranks) / wall time.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+WIDTH, HEIGHT, SPP, DEPTH = 1920, 1080, 8, 8
+KNOT = (350, 100)  # 70,000 triangles: the ~70k-triangle bunny stand-in
+CAMERA = dict(pitch=0.08, radius=12.5, center=(0.0, 1.2, 0.0))
+BAND_ROWS = 8
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(counts: dict, sphere_count: int, leaf_size: int, pixels: int, passes: int) -> float:
+    """SURVEY.md §8(d) per-segment byte model in the reference's data layout:
+    100 B path state per segment (alive index 4, ray in 24, scattering 24, throughput R/W 24,
+    ray out 24) + 16 B per sphere + 32 B per BVH node + 4 B per leaf slot + 36 B per triangle test
+    + 120 B per mesh hit (normals 36, material 84) + 84 B per sphere hit + 16 B (bilinear sky) and
+    24 B (radiance R/W) per miss; plus 115 B per pixel per pass (init, raygen, gamma, 8-bit)."""
+    seg = counts["segments"]
+    b = (100.0 * seg + 16.0 * sphere_count * seg + 32.0 * counts["nodes"] + 4.0 * counts["tris"] * (1 if leaf_size == 1 else 1)
+         + 36.0 * counts["tris"] + 120.0 * counts["hit_mesh"] + 84.0 * counts["hit_sphere"] + 40.0 * counts["miss"])
+    return b + 115.0 * pixels * passes
+
+
+def cpu_baseline(scene, cam, cfg, threads: int) -> dict:
+    """The reference's CPU fallback semantics (Core/path_tracer_cpu.cpp: MSVC rand, libm), as
+    restated by the oracle, on the same frame: a bounded sample of two passes."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # cpu_baseline leg only
+
+    oracle.lib()
+    t0 = time.perf_counter()
+    _, _, st = oracle.render(scene.view, cam, cfg, 1, 2, rng="msvc", math="libm", threads=threads, with_u8=True)
+    dt = time.perf_counter() - t0
+    return {"value": round(st["segments"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"passes 1-2 of the {WIDTH}x{HEIGHT} depth-{DEPTH} frame (all pixels, {st['segments']} ray "
+                      f"segments, {dt:.2f} s), oracle in reference-CPU-fallback mode (MSVC rand, libm)",
+            "ms_per_frame_extrapolated": round(dt / 2 * SPP * 1000, 1)}
+
+
+def load_traffic(workload: str):
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        e = d.get(workload)
+        return float(e["hbm_bytes_per_launch"]) if e else None
+    except Exception:
+        return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--save-image", default="")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE {world}: launch N>1 with torch.distributed.run",
+              file=sys.stderr)
+        if world == 1 and args.gpus > 1:
+            return 2
+
+    import torch
+    import torch.distributed as dist
+
+    import pathtracerwithcuda_amd as pt
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    r = pt.Renderer(local)
+    scene = pt.cornell_scene(pt.torus_knot(*KNOT))
+    cfg = pt.configuration(max_tracer_depth=DEPTH)
+    cam = pt.camera(WIDTH, HEIGHT, **CAMERA)
+    r.upload(scene, cfg)
+    image = None
+    if world > 1:
+        image = torch.zeros(WIDTH * HEIGHT * 3, dtype=torch.float32, device=f"cuda:{local}")
+        r.setup_frame(WIDTH, HEIGHT, image.data_ptr())
+        r.set_tiling(BAND_ROWS, world, rank)
+    else:
+        r.setup_frame(WIDTH, HEIGHT)
+
+    def frame():
+        r.render(cam, cfg, 1, SPP, write_u8=2 if world == 1 else 0)
+        if world > 1:
+            r.synchronize()
+            dist.reduce(image, dst=0)  # RCCL over xGMI: the one collective of the frame
+            if rank == 0:
+                torch.cuda.synchronize()
+                r.finalize_u8(cfg, SPP)
+        r.synchronize()
+
+    # roofline inputs: one instrumented (untimed) frame for the visit counts
+    r.set_instrumented(True)
+    r.stats_reset()
+    r.render(cam, cfg, 1, SPP, write_u8=0)
+    r.synchronize()
+    counts = r.stats_all()
+    r.set_instrumented(False)
+
+    for _ in range(args.warmup):
+        frame()
+    r.stats_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    segments = r.stats()["segments"]
+    kernel_ms, launches = r.kernel_time()
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        s = torch.tensor([segments], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(s)
+        segments = int(s.item())
+        c = torch.tensor([counts[k] for k in sorted(counts)], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(c)
+        counts = {k: int(v) for k, v in zip(sorted(counts), c.tolist())}
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
+
+    if args.save_image:
+        from pathtracerwithcuda_amd.imageio import write_png
+        _, img8 = r.download()
+        write_png(args.save_image, img8)
+
+    value = segments / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1000.0
+    avg_launch_s = kernel_ms / max(launches, 1) / 1000.0
+    # one launch = one pass over the frame (this rank's bands when tiled)
+    bytes_per_launch = algorithmic_bytes(counts, scene.view.sphere_num, cfg.bvh_leaf_node_triangle_num,
+                                         WIDTH * HEIGHT, SPP) / SPP / world
+    achieved = bytes_per_launch / avg_launch_s / 1e9
+    workload = f"cornell+knot{KNOT[0] * KNOT[1] * 2}_{WIDTH}x{HEIGHT}_spp{SPP}_d{DEPTH}"
+    traffic = load_traffic(workload)
+    line = {
+        "metric": "Mrays/sec + ms/frame @1920x1080, 8spp, 8-bounce; 1/2/4/8 GPU",
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: procedural 70k-triangle torus knot (bunny stand-in) + procedural 512^2 cube map",
+        "config": {
+            "workload": workload,
+            "scene": "Cornell box (cornell.obj walls, cube.obj light, iron+glass spheres) + torus knot, "
+                     f"{scene.triangle_count} triangles, {scene.view.sphere_num} spheres",
+            "width": WIDTH, "height": HEIGHT, "spp": SPP, "max_depth": DEPTH,
+            "parallelism": f"tiled{world}" if world > 1 else "single",
+            "band_rows": BAND_ROWS if world > 1 else None,
+            "ms_per_frame": round(ms_per_step, 3),
+            "camera_samples_per_s_M": round(WIDTH * HEIGHT * SPP * args.steps / elapsed / 1e6, 3),
+            "segments_per_frame": segments // max(args.steps, 1),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "pass_kernel<LEAF1=true,STATS=false>",
+            "avg_launch_ms": round(avg_launch_s * 1000, 4),
+            "algorithmic_bytes_per_launch": round(bytes_per_launch),
+            "counts_per_frame": counts,
+        },
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        line["cpu_baseline"] = cpu_baseline(scene, cam, cfg, threads)
+        line["cpu_baseline"]["cpu"] = platform.processor() or platform.machine()
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

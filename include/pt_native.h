@@ -1,0 +1,83 @@
+/*
+ * pt_native.h — native C-ABI of libpt_hip.so underneath the reference boundary.
+ *
+ * The reference ABI (path_tracer_kernel.h) is one synchronous pass per call on host-visible
+ * memory. This API keeps the scene and the accumulation image resident in HBM, renders any
+ * number of passes per call on one HIP stream, and exposes what the benchmark and the multi-GPU
+ * driver need (tiling, device image pointer, counters, event timing). Every function returns
+ * PT_OK (0) or a negative PT_E* code; pt_last_error() describes the last failure.
+ */
+#ifndef PT_NATIVE_H
+#define PT_NATIVE_H
+
+#include "pt_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_OK 0
+#define PT_E_ARG (-1)
+#define PT_E_HIP (-2)
+#define PT_E_STATE (-3)
+#define PT_E_NOMEM (-4)
+
+typedef struct pt_context pt_context;
+
+const char* pt_last_error(void);
+int pt_device_count(void);
+
+int pt_context_create(int device, pt_context** out);
+void pt_context_destroy(pt_context* ctx);
+
+/* Translate reference-layout, host-readable scene structures into the device layout and upload
+ * them (relocating triangle.mat, node.triangle_indices, cube-map faces and texture pixels).
+ * triangle_num / texture_num < 0: derive them from the BVH leaves / material texture ids. */
+int pt_scene_upload(pt_context* ctx, int mesh_num, pt_bvh_node_device** bvh_nodes, pt_triangle* triangles,
+                    int triangle_num, int sphere_num, pt_sphere* spheres, pt_cube_map* sky_cube_map,
+                    pt_texture_wrapper* mesh_textures, int texture_num, const pt_configuration* config);
+/* Device bytes of the resident scene and its node / triangle counts. */
+int pt_scene_info(pt_context* ctx, long long* device_bytes, int* node_num, int* triangle_num);
+
+/* Frame geometry. The image is width*height float3 (12 B/pixel) + uchar3, device resident.
+ * image_device: optional caller-owned device buffer (e.g. a torch tensor used for the RCCL
+ * reduce); NULL = the context allocates its own. */
+int pt_frame_setup(pt_context* ctx, int width, int height, void* image_device);
+/* Own only the rows y with (y / band_rows) % band_count == band_index (multi-GPU tiling). */
+int pt_set_tiling(pt_context* ctx, int band_rows, int band_count, int band_index);
+
+/* Render passes first_pass .. first_pass+pass_count-1 (pass_counter semantics of the reference:
+ * pass 1 overwrites the image, later passes add). write_u8: 0 never, 1 every pass, 2 last pass.
+ * Asynchronous on the context stream. */
+int pt_render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config,
+                     int first_pass, int pass_count, int write_u8);
+/* 8-bit gamma output of the current image for `pass` accumulated passes (after an external reduce). */
+int pt_finalize_u8(pt_context* ctx, const pt_configuration* config, int pass);
+int pt_synchronize(pt_context* ctx);
+
+int pt_image_download(pt_context* ctx, pt_float3* image, pt_uchar3* image256);
+void* pt_image_device_ptr(pt_context* ctx);
+void* pt_image256_device_ptr(pt_context* ctx);
+
+/* Counters since the last pt_stats_reset: ray segments (sum of live rays over every trace step,
+ * the reference's thread_shrink inputs), BVH nodes visited and triangle tests (instrumented
+ * kernel only, see pt_set_instrumented). */
+int pt_stats_reset(pt_context* ctx);
+int pt_stats(pt_context* ctx, unsigned long long* segments, unsigned long long* nodes, unsigned long long* tris);
+/* All counters: [0] segments, [1] nodes, [2] triangle tests, [3] mesh hits, [4] sphere hits,
+ * [5] misses, [6] subsurface scatter events ([1..6] instrumented kernel only). n <= 32. */
+int pt_stats_all(pt_context* ctx, unsigned long long* out, int n);
+int pt_set_instrumented(pt_context* ctx, int on);
+/* HIP-event time of the pass kernels since the last pt_stats_reset (on the stream they run on). */
+int pt_kernel_time(pt_context* ctx, double* total_ms, int* launches);
+
+/* Diagnostic: evaluate the device transcendentals (which: 0 sincos, 1 exp, 2 log, 3 atan, 4 asin,
+ * 5 acos, 6 pow(x,1.85), 7 tan, 8 sqrt & reciprocal) on n host floats; for the bitwise check
+ * against the oracle's host restatement. */
+int pt_math_eval_device(pt_context* ctx, int which, const float* x, int n, float* out0, float* out1);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PT_NATIVE_H */

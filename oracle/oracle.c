@@ -1,0 +1,626 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE: the CPU restatement of the reference's per-pass radiance
+ * loop that the HIP path is checked against. Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load it; the product never links or calls it.
+ *
+ * Structure follows the reference CPU fallback (Core/path_tracer_cpu.cpp:634-722) — per-pixel
+ * arrays, an alive list compacted after every depth (thread_shrink = stable remove_if) — and
+ * its arithmetic follows the GPU kernel (Kernel/path_tracer_kernel.cu), with two switches:
+ *   rng  OR_RNG_THRUST (0): thrust::default_random_engine (minstd_rand) +
+ *                           uniform_real_distribution<float>, seeded as the GPU kernel seeds it
+ *                           (:324, :415). Pinned by tests/golden/rng_*.json, generated from
+ *                           rocThrust (the same Thrust algorithm as CUDA 9.1's).
+ *        OR_RNG_MSVC   (1): srand/rand with MSVC CRT semantics (RAND_MAX 0x7fff), seeded as
+ *                           path_tracer_cpu.cpp:285,368 — the reference CPU fallback itself.
+ *   math OR_MATH_CEPHES / OR_MATH_LIBM (oracle_math.h).
+ * Scene input is the reference's own data layout (include/pt_types.h): triangle.mat and
+ * bvh_node_device.triangle_indices are dereferenced exactly as the reference does.
+ */
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/pt_types.h"
+#include "oracle_math.h"
+
+#define OR_RNG_THRUST 0
+#define OR_RNG_MSVC 1
+
+/* path_tracer_kernel.cu:35-44 / path_tracer_cpu.cpp:3-12 (int with wrap-around, arithmetic >>) */
+int32_t or_hash(int32_t a_in) {
+    uint32_t a = (uint32_t)a_in;
+    a = (a + 0x7ed55d16u) + (a << 12);
+    a = (a ^ 0xc761c23cu) ^ (uint32_t)((int32_t)a >> 19);
+    a = (a + 0x165667b1u) + (a << 5);
+    a = (a + 0xd3a2646cu) ^ (a << 9);
+    a = (a + 0xfd7046c5u) + (a << 3);
+    a = (a ^ 0xb55a4f09u) ^ (uint32_t)((int32_t)a >> 16);
+    return (int32_t)a;
+}
+
+static int32_t mulw(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+
+typedef struct { uint32_t x; int kind; } or_rng;
+
+/* thrust linear_congruential_engine<uint32, 48271, 0, 2147483647>::seed / operator() */
+static or_rng rng_seed(int kind, int32_t s) {
+    or_rng r;
+    r.kind = kind;
+    if (kind == OR_RNG_THRUST) {
+        uint32_t v = (uint32_t)s % 2147483647u;
+        r.x = v ? v : 1u;
+    } else {
+        r.x = (uint32_t)s;  /* MSVC srand */
+    }
+    return r;
+}
+static uint32_t minstd_next(or_rng* r) {
+    r->x = (uint32_t)(((uint64_t)r->x * 48271u) % 2147483647u);
+    return r->x;
+}
+/* uniform_real_distribution<float>(a, b)::operator() (uniform_real_distribution.inl:67-79) */
+static float thrust_uniform(or_rng* r, float a, float b) {
+    float res = (float)(minstd_next(r) - 1u);
+    res = res / (1.0f + (float)(2147483646u - 1u));
+    return res * (b - a) + a;
+}
+static int msvc_rand(or_rng* r) {
+    r->x = r->x * 214013u + 2531011u;
+    return (int)((r->x >> 16) & 0x7fffu);
+}
+/* draws used by trace_ray: uniform(0,1) | rand()/RAND_MAX */
+static float draw01(or_rng* r) {
+    if (r->kind == OR_RNG_THRUST) return thrust_uniform(r, 0.0f, 1.0f);
+    return (float)msvc_rand(r) / 32767;
+}
+/* anti-alias jitter (:333-334 | cpu :291-292) */
+static float draw_jitter(or_rng* r) {
+    if (r->kind == OR_RNG_THRUST) return thrust_uniform(r, -0.5f, 0.5f);
+    return ((float)msvc_rand(r) / 32767) - 0.5f;
+}
+/* aperture sample (:358-359 | cpu :314-315) */
+static float draw_aperture(or_rng* r) {
+    if (r->kind == OR_RNG_THRUST) return thrust_uniform(r, -0.5f, 0.5f) + 0.5f;
+    return (float)msvc_rand(r) / 32767;
+}
+
+/* exported for the RNG golden-vector tests */
+void or_rng_stream(int kind, int32_t seed, int n, float a, float b, float* out) {
+    or_rng r = rng_seed(kind, seed);
+    for (int i = 0; i < n; i++) out[i] = kind == OR_RNG_THRUST ? thrust_uniform(&r, a, b) : (float)msvc_rand(&r);
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+static or_v3 f3(pt_float3 a) { return v3(a.x, a.y, a.z); }
+static pt_float3 pf3(or_v3 a) { pt_float3 r; r.x = a.x; r.y = a.y; r.z = a.z; return r; }
+
+typedef struct {
+    int mesh_num;
+    pt_bvh_node_device** bvh;
+    const pt_triangle* tris;
+    int sphere_num;
+    const pt_sphere* spheres;
+    const pt_cube_map* cube;
+    const pt_texture_wrapper* textures;
+    const pt_configuration* cfg;
+    int math;
+} or_scene;
+
+typedef struct { unsigned long long nodes, tris; } or_counts;
+
+/* path_tracer_kernel.cu:46-52 */
+static or_v3 reflection(or_v3 n, or_v3 in) { return v_sub(in, s_scale(2.0f * v_dot(n, in), n)); }
+
+/* :54-83 */
+static or_v3 refraction(or_v3 n, or_v3 in, float in_n, float out_n) {
+    or_v3 i = v_scale(in, -1.0f);
+    float ndi = v_dot(n, i);
+    float ratio = in_n / out_n;
+    float a = ratio * ndi;
+    float b = 1.0f - ratio * ratio * (1.0f - ndi * ndi);
+    if (b < 0.0f) return v3(0.0f, 0.0f, 0.0f);
+    if (ndi > 0) return v_sub(v_scale(n, a - sqrtf(b)), s_scale(ratio, i));
+    return v_sub(v_scale(n, a + sqrtf(b)), s_scale(ratio, i));
+}
+
+/* Core/sphere.h:18-55 */
+static int sphere_intersect(const pt_sphere* s, or_v3 o, or_v3 d, or_v3* hp, or_v3* hn, float* ht) {
+    or_v3 op = v_sub(f3(s->center), o);
+    float b = v_dot(op, d);
+    float delta = b * b - v_dot(op, op) + s->radius * s->radius;
+    if (delta < 0) return 0;
+    float dr = sqrtf(delta);
+    float t1 = b - dr, t2 = b + dr;
+    if (t1 < 0 && t2 < 0) return 0;
+    if (t1 > 0 && t2 > 0) *ht = fminf(t1, t2);
+    else *ht = fmaxf(t1, t2);
+    *hp = v_add(o, v_scale(d, *ht));
+    *hn = v_norm(v_sub(*hp, f3(s->center)));
+    return 1;
+}
+
+/* Core/triangle.h:27-62 */
+static int triangle_intersect(const pt_triangle* t, or_v3 o, or_v3 d, float* ht, float* ht1, float* ht2) {
+    or_v3 v0 = f3(t->vertex0);
+    or_v3 e1 = v_sub(f3(t->vertex1), v0);
+    or_v3 e2 = v_sub(f3(t->vertex2), v0);
+    or_v3 p = v_cross(d, e2);
+    float det = v_dot(e1, p);
+    if (det == 0.0f) return 0;
+    float inv = 1.0f / det;
+    or_v3 tv = v_sub(o, v0);
+    or_v3 q = v_cross(tv, e1);
+    float t1 = v_dot(tv, p) * inv;
+    float t2 = v_dot(d, q) * inv;
+    float tt = v_dot(e2, q) * inv;
+    if (t1 >= 0.0f && t2 >= 0.0f && t1 + t2 <= 1.0f) { *ht = tt; *ht1 = t1; *ht2 = t2; return 1; }
+    return 0;
+}
+
+/* Bvh/bounding_box.h:83-102 */
+static int box_intersect(const pt_bounding_box* b, or_v3 o, or_v3 d, float* hit_t) {
+    or_v3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    float tx1 = (b->left_bottom.x - o.x) * inv.x, tx2 = (b->right_top.x - o.x) * inv.x;
+    float ty1 = (b->left_bottom.y - o.y) * inv.y, ty2 = (b->right_top.y - o.y) * inv.y;
+    float tz1 = (b->left_bottom.z - o.z) * inv.z, tz2 = (b->right_top.z - o.z) * inv.z;
+    float t_max = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    float t_min = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    int is_hit = t_max <= t_min;
+    if (is_hit) *hit_t = t_max;
+    return is_hit && t_min > 0.0f;
+}
+
+/* path_tracer_kernel.cu:85-161 */
+static int mesh_bvh(const or_scene* sc, int m, or_v3 o, or_v3 d, float* ht, float* ht1, float* ht2, int* htri,
+                    or_counts* cnt) {
+    float min_t = INFINITY, min_t1 = INFINITY, min_t2 = INFINITY;
+    int min_tri = -1, hit = 0;
+    float box_t = INFINITY;
+    const pt_bvh_node_device* nodes = sc->bvh[m];
+    int node_num = nodes[0].next_node_index;
+    int pos = 0;
+    while (pos != node_num) {
+        const pt_bvh_node_device* n = &nodes[pos];
+        cnt->nodes++;
+        if (box_intersect(&n->box, o, d, &box_t) && box_t <= min_t) {
+            if (n->is_leaf) {
+                for (int i = 0; i < sc->cfg->bvh_leaf_node_triangle_num; i++) {
+                    int ti = n->triangle_indices[i];
+                    if (ti == -1) break;
+                    float t, t1, t2;
+                    cnt->tris++;
+                    if (triangle_intersect(&sc->tris[ti], o, d, &t, &t1, &t2) && t > 0.0f && t < min_t) {
+                        min_t = t; min_t1 = t1; min_t2 = t2; min_tri = ti; hit = 1;
+                    }
+                }
+            }
+            pos++;
+        } else {
+            pos = n->next_node_index;
+        }
+    }
+    if (hit) { *ht = min_t; *ht1 = min_t1; *ht2 = min_t2; *htri = min_tri; }
+    return hit;
+}
+
+/* the orthonormal basis of :174-189 (abs on float -> fabsf) */
+static void frame(or_v3 n, or_v3* vi, or_v3* vj) {
+    or_v3 any;
+    if (fabsf(n.x) < OR_SQRT_ONE_THIRD) any = v3(1.0f, 0.0f, 0.0f);
+    else if (fabsf(n.y) < OR_SQRT_ONE_THIRD) any = v3(0.0f, 1.0f, 0.0f);
+    else any = v3(0.0f, 0.0f, 1.0f);
+    *vi = v_norm(v_cross(n, any));
+    *vj = v_cross(n, *vi);
+}
+
+/* :163-192 */
+static or_v3 hemisphere_cosine(int mm, or_v3 n, float r1, float r2) {
+    float ct = sqrtf(r1);
+    float st = sqrtf(1.0f - ct * ct);
+    float phi = r2 * OR_TWO_PI;
+    or_v3 vi, vj;
+    frame(n, &vi, &vj);
+    float sp, cp;
+    m_sincos(mm, phi, &sp, &cp);
+    return v_add(v_add(s_scale(ct, n), s_scale(cp * st, vi)), s_scale(sp * st, vj));
+}
+
+/* :194-223 */
+static or_v3 hemisphere_ggx(int mm, or_v3 n, float rough, float r1, float r2) {
+    float theta = m_atan(mm, rough * sqrtf(r1) / sqrtf(1.0f - r1));
+    float phi = r2 * OR_TWO_PI;
+    float st, ct;
+    m_sincos(mm, theta, &st, &ct);
+    or_v3 vi, vj;
+    frame(n, &vi, &vj);
+    float sp, cp;
+    m_sincos(mm, phi, &sp, &cp);
+    return v_add(v_add(s_scale(ct, n), s_scale(cp * st, vi)), s_scale(sp * st, vj));
+}
+
+/* :225-236 */
+static or_v3 on_sphere(int mm, float r1, float r2) {
+    float ct = r1 * 2.0f - 1.0f;
+    float st = sqrtf(1.0f - ct * ct);
+    float phi = r2 * OR_TWO_PI;
+    float sp, cp;
+    m_sincos(mm, phi, &sp, &cp);
+    return v3(ct, cp * st, sp * st);
+}
+
+/* :238-249 */
+static or_v3 absorption_through(int mm, pt_float3 a, float d) {
+    return v3(m_exp(mm, -1.0f * a.x * d), m_exp(mm, -1.0f * a.y * d), m_exp(mm, -1.0f * a.z * d));
+}
+
+/* :251-273 */
+static float ggx_masking(float rough, or_v3 macro, or_v3 micro, or_v3 dir) {
+    or_v3 v = s_scale(-1.0f, dir);
+    float vdn = v_dot(v, macro), vdm = v_dot(v, micro);
+    float positive = (vdm / vdn) > 0.0f ? 1.0f : 0.0f;
+    if (positive == 0.0f) return 0.0f;
+    float r2 = rough * rough;
+    float c2 = vdn * vdn;
+    float t2 = (1.0f - c2) / c2;
+    return 2.0f / (1.0f + sqrtf(1.0f + r2 * t2));
+}
+
+/* Core/fresnel.h:11-49 */
+static float fresnel_dielectrics(int mm, or_v3 n, or_v3 in, float in_n, float out_n, or_v3 refr) {
+    float cin = v_dot(n, v_scale(in, -1.0f));
+    float cout = v_dot(s_scale(-1.0f, n), refr);
+    if (in_n > out_n && m_acos(mm, cin) >= m_asin(mm, out_n / in_n)) return 1.0f;
+    if (v_len(refr) <= 0.000005f || cout < 0) return 1.0f;
+    float s = (in_n * cin - out_n * cout) / (in_n * cin + out_n * cout);
+    float p = (in_n * cout - out_n * cin) / (in_n * cout + out_n * cin);
+    return (s * s + p * p) / 2.0f;
+}
+
+/* Core/fresnel.h:51-76 */
+static float fresnel_conductors(or_v3 n, or_v3 in, float eta, float k) {
+    float cin = v_dot(n, v_scale(in, -1.0f));
+    float nk = eta * eta + k * k;
+    float c2 = cin * cin;
+    float tnc = 2 * eta * cin;
+    float rs = (nk * c2 - tnc + 1.0f) / (nk * c2 + tnc + 1.0f);
+    float rp = (nk - tnc + c2) / (nk + tnc + c2);
+    return (rs + rp) / 2.0f;
+}
+
+static or_v3 px_color(const unsigned char* px, int i) {
+    return v3(px[i * 4 + 0] / 255.0f, px[i * 4 + 1] / 255.0f, px[i * 4 + 2] / 255.0f);
+}
+
+/* Core/texture.h:15-79 and the face lookup of Core/cube_map.h:28-104 */
+static or_v3 sample_image(const unsigned char* px, int w, int h, float u, float v, int bilinear) {
+    if (bilinear) {
+        float xr = u * (float)(w - 1), yr = (1.0f - v) * (float)(h - 1);
+        int fx = (int)or_clamp(floorf(xr), 0.0f, (float)(w - 1));
+        int cx = (int)or_clamp(ceilf(xr), 0.0f, (float)(w - 1));
+        int fy = (int)or_clamp(floorf(yr), 0.0f, (float)(h - 1));
+        int cy = (int)or_clamp(ceilf(yr), 0.0f, (float)(h - 1));
+        float lr = xr - floorf(xr), bt = yr - floorf(yr);
+        or_v3 c0 = px_color(px, fy * w + fx), c1 = px_color(px, fy * w + cx);
+        or_v3 c2 = px_color(px, cy * w + fx), c3 = px_color(px, cy * w + cx);
+        return v_lerp(v_lerp(c0, c1, lr), v_lerp(c2, c3, lr), bt);
+    }
+    int x = (int)or_clamp(u * (float)(w - 1), 0.0f, (float)(w - 1));
+    int y = (int)or_clamp((1.0f - v) * (float)(h - 1), 0.0f, (float)(h - 1));
+    return px_color(px, y * w + x);
+}
+
+/* Math/cuda_math.hpp:56-126 */
+static void cube_uv(float x, float y, float z, int* index, float* u, float* v) {
+    float ax = fabsf(x), ay = fabsf(y), az = fabsf(z);
+    int xp = x > 0, yp = y > 0, zp = z > 0;
+    float maxa = 1.0f, uc = 0.0f, vc = 0.0f;
+    int idx = 0;
+    if (xp && ax >= ay && ax >= az) { maxa = ax; uc = -z; vc = y; idx = 0; }
+    if (!xp && ax >= ay && ax >= az) { maxa = ax; uc = z; vc = y; idx = 1; }
+    if (yp && ay >= ax && ay >= az) { maxa = ay; uc = x; vc = -z; idx = 2; }
+    if (!yp && ay >= ax && ay >= az) { maxa = ay; uc = x; vc = z; idx = 3; }
+    if (zp && az >= ax && az >= ay) { maxa = az; uc = x; vc = y; idx = 4; }
+    if (!zp && az >= ax && az >= ay) { maxa = az; uc = -x; vc = y; idx = 5; }
+    *u = 0.5f * (uc / maxa + 1.0f);
+    *v = 0.5f * (vc / maxa + 1.0f);
+    *index = idx;
+}
+
+/* Core/cube_map.h:20-119 */
+static or_v3 background(const or_scene* sc, or_v3 d) {
+    const pt_configuration* c = sc->cfg;
+    if (c->use_sky_box) {
+        if (!sc->cube || sc->cube->length <= 0) return v3(0.0f, 0.0f, 0.0f);
+        float u, v;
+        int f;
+        cube_uv(d.x, d.y, d.z, &f, &u, &v);
+        const unsigned char* faces[6] = {sc->cube->m_x_positive_map, sc->cube->m_x_negative_map,
+                                         sc->cube->m_y_positive_map, sc->cube->m_y_negative_map,
+                                         sc->cube->m_z_positive_map, sc->cube->m_z_negative_map};
+        return sample_image(faces[f], sc->cube->length, sc->cube->length, u, v, c->use_bilinear);
+    }
+    if (c->use_sky) {
+        float t = (v_dot(d, v3(-0.41f, 0.41f, -0.82f)) + 1.0f) / 2.0f;
+        or_v3 a = v3(0.15f, 0.3f, 0.5f), b = v3(1.0f, 1.0f, 1.0f);
+        return v_scale(v_add(s_scale(1.0f - t, a), s_scale(t, b)), 1.0f);
+    }
+    return v3(0.0f, 0.0f, 0.0f);
+}
+
+/* per-pixel state of the reference (path_tracer_kernel.h:18-37 scratch arrays) */
+typedef struct {
+    int* alive;            /* energy_exist_pixels: entries index the state arrays */
+    pt_ray* rays;
+    or_v3* thr;            /* not_absorbed_colors */
+    or_v3* rad;            /* accumulated_colors */
+    pt_scattering* sca;    /* scatterings */
+} or_state;
+
+/* init_data (:275-297) + generate_ray (:299-379 | cpu :264-339) for state slot k = pixel */
+static void generate(const or_scene* sc, const pt_render_camera* cam, int rng_kind, int seed, int k, int pixel,
+                     or_state* st) {
+    const pt_configuration* cfg = sc->cfg;
+    int mm = sc->math;
+    st->alive[k] = k;
+    st->thr[k] = v3(1.0f, 1.0f, 1.0f);
+    st->rad[k] = v3(0.0f, 0.0f, 0.0f);
+    st->sca[k].absorption_coefficient = cfg->air_absorption_coef;
+    st->sca[k].reduced_scattering_coefficient = cfg->air_reduced_scattering_coef;
+
+    float rx = cam->resolution.x, ry = cam->resolution.y;
+    int image_y = (int)((float)pixel / rx);
+    int image_x = (int)((float)pixel - ((float)image_y * rx));
+    int32_t hs = or_hash(seed);
+    or_rng rng = rng_seed(rng_kind, mulw(mulw(hs, hs), or_hash(pixel)));
+    float jx = 0.0f, jy = 0.0f;
+    if (cfg->use_anti_alias) { jx = draw_jitter(&rng); jy = draw_jitter(&rng); }
+    or_v3 eye = f3(cam->eye), view = f3(cam->view), up = f3(cam->up);
+    float distance = v_len(view);
+    or_v3 hz = v_norm(v_cross(view, up));
+    or_v3 vt = v_norm(v_cross(hz, view));
+    or_v3 xa = v_scale(hz, distance * m_tan(mm, cam->fov.x * 0.5f * (OR_PI / 180.0f)));
+    or_v3 ya = v_scale(vt, distance * m_tan(mm, -cam->fov.y * 0.5f * (OR_PI / 180.0f)));
+    float nx = (((float)image_x + jx) / (rx - 1.0f)) * 2.0f - 1.0f;
+    float ny = (((float)image_y + jy) / (ry - 1.0f)) * 2.0f - 1.0f;
+    or_v3 canvas = v_add(v_add(v_add(eye, view), s_scale(nx, xa)), s_scale(ny, ya));
+    or_v3 image_plane = v_add(eye, v_scale(v_norm(v_sub(canvas, eye)), cam->focal_distance));
+    or_v3 ap;
+    if (cam->aperture_radius > 0.00001f) {
+        float r1 = draw_aperture(&rng), r2 = draw_aperture(&rng);
+        float angle = r1 * OR_TWO_PI;
+        float dist = cam->aperture_radius * sqrtf(r2);
+        float sa, ca;
+        m_sincos(mm, angle, &sa, &ca);
+        ap = v_add(v_add(eye, s_scale(ca * dist, hz)), s_scale(sa * dist, vt));
+    } else {
+        ap = eye;
+    }
+    st->rays[k].origin = pf3(ap);
+    st->rays[k].direction = pf3(v_norm(v_sub(image_plane, ap)));
+}
+
+/* trace_ray_kernel (:381-625 | cpu :341-578) for alive-list entry ai */
+static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const int* pixel_of, int ai, or_state* st,
+                  or_counts* cnt) {
+    const pt_configuration* cfg = sc->cfg;
+    int mm = sc->math;
+    int k = st->alive[ai];
+    int pixel = pixel_of ? pixel_of[k] : k;
+    or_v3 o = f3(st->rays[k].origin), d = f3(st->rays[k].direction);
+    or_rng rng = rng_seed(rng_kind, mulw(mulw(or_hash(seed), or_hash(pixel)), or_hash(depth)));
+
+    float ht, ht1, ht2;
+    or_v3 hp, hn;
+    int htri;
+    float min_t = INFINITY, min_t1 = INFINITY, min_t2 = INFINITY;
+    or_v3 min_point = v3(0, 0, 0), min_normal = v3(0, 0, 0);
+    int type = 0, min_sphere = -1, min_tri = -1;
+
+    for (int i = 0; i < sc->sphere_num; i++) {
+        if (sphere_intersect(&sc->spheres[i], o, d, &hp, &hn, &ht) && ht < min_t && ht > 0.0f) {
+            min_t = ht; min_point = hp; min_normal = hn; min_sphere = i; type = 1;
+        }
+    }
+    for (int m = 0; m < sc->mesh_num; m++) {
+        if (mesh_bvh(sc, m, o, d, &ht, &ht1, &ht2, &htri, cnt) && ht < min_t && ht > 0.0f) {
+            min_t = ht; min_t1 = ht1; min_t2 = ht2;
+            min_point = v_add(o, v_scale(d, ht));
+            min_tri = htri; type = 2;
+        }
+    }
+
+    pt_scattering cs = st->sca[k];
+    if (cs.reduced_scattering_coefficient.x > 0.0f || v_len(f3(cs.absorption_coefficient)) > cfg->sss_threshold) {
+        float r = draw01(&rng);
+        float dist = -m_log(mm, r) / cs.reduced_scattering_coefficient.x;
+        if (dist < min_t) {
+            float r1 = draw01(&rng), r2 = draw01(&rng);
+            st->rays[k].origin = pf3(v_add(o, v_scale(d, dist)));
+            st->rays[k].direction = pf3(on_sphere(mm, r1, r2));
+            st->thr[k] = v_mul(st->thr[k], absorption_through(mm, cs.absorption_coefficient, dist));
+            if (v_len(st->thr[k]) <= cfg->energy_exist_threshold) st->alive[ai] = -1;
+            return;
+        }
+        st->thr[k] = v_mul(st->thr[k], absorption_through(mm, cs.absorption_coefficient, min_t));
+    }
+
+    if (type == 0) {
+        or_v3 bg = background(sc, d);
+        st->rad[k] = v_add(st->rad[k], v_mul(st->thr[k], bg));
+        st->alive[ai] = -1;
+        return;
+    }
+
+    pt_material mat;
+    if (type == 1) {
+        mat = sc->spheres[min_sphere].mat;
+    } else {
+        const pt_triangle* tr = &sc->tris[min_tri];
+        mat = *tr->mat;
+        float w = 1.0f - min_t1 - min_t2;
+        min_normal = v_add(v_add(v_scale(f3(tr->normal0), w), v_scale(f3(tr->normal1), min_t1)),
+                           v_scale(f3(tr->normal2), min_t2));
+        float u = 0.0f, v = 0.0f;
+        if (mat.diffuse_texture_id != -1 || mat.specular_texture_id != -1) {
+            u = (tr->uv0.x * w + tr->uv1.x * min_t1) + tr->uv2.x * min_t2;
+            v = (tr->uv0.y * w + tr->uv1.y * min_t1) + tr->uv2.y * min_t2;
+        }
+        float au = u - floorf(u), av = v - floorf(v);
+        if (mat.diffuse_texture_id != -1) {
+            const pt_texture_wrapper* t = &sc->textures[mat.diffuse_texture_id];
+            or_v3 c = sample_image(t->pixels, t->width, t->height, au, av, cfg->use_bilinear);
+            mat.diffuse_color = pf3(v_mul(f3(mat.diffuse_color), c));
+        }
+        if (mat.specular_texture_id != -1) {
+            const pt_texture_wrapper* t = &sc->textures[mat.specular_texture_id];
+            or_v3 c = sample_image(t->pixels, t->width, t->height, au, av, cfg->use_bilinear);
+            mat.specular_color = pf3(v_mul(f3(mat.specular_color), c));
+        }
+    }
+
+    float in_n = cfg->air_refraction_index;
+    pt_scattering in_sca, out_sca;
+    in_sca.absorption_coefficient = cfg->air_absorption_coef;
+    in_sca.reduced_scattering_coefficient = cfg->air_reduced_scattering_coef;
+    float out_n = mat.medium.refraction_index;
+    out_sca = mat.medium.scattering;
+    if (v_dot(d, min_normal) > 0) {
+        min_normal = v_scale(min_normal, -1.0f);
+        if (mat.is_transparent) {
+            float tn = in_n; in_n = out_n; out_n = tn;
+            pt_scattering ts = in_sca; in_sca = out_sca; out_sca = ts;
+        }
+    }
+    or_v3 refr = refraction(min_normal, d, in_n, out_n);
+    or_v3 bias = s_scale(cfg->vector_bias_length, min_normal);
+    float R;
+    if (mat.medium.extinction_coefficient == 0 || mat.is_transparent) R = fresnel_dielectrics(mm, min_normal, d, in_n, out_n, refr);
+    else R = fresnel_conductors(min_normal, d, out_n, mat.medium.extinction_coefficient);
+
+    float r = draw01(&rng);
+    if (r < R) {
+        float r1 = draw01(&rng), r2 = draw01(&rng);
+        float rough = m_pow(mm, mat.roughness, 1.85f) * 0.238f;
+        or_v3 micro = hemisphere_ggx(mm, min_normal, rough, r1, r2);
+        or_v3 mr = reflection(micro, d);
+        float shadow = ggx_masking(rough, min_normal, micro, d) * ggx_masking(rough, min_normal, micro, mr);
+        st->rays[k].origin = pf3(v_add(min_point, bias));
+        st->rays[k].direction = pf3(mr);
+        st->thr[k] = v_mul(st->thr[k], v_scale(f3(mat.specular_color), shadow));
+    } else if (mat.is_transparent) {
+        st->rays[k].origin = pf3(v_sub(min_point, bias));
+        st->rays[k].direction = pf3(refr);
+        st->sca[k] = out_sca;
+        float ratio = out_n / in_n;
+        st->thr[k] = v_scale(st->thr[k], ratio * ratio);
+    } else {
+        st->rad[k] = v_add(st->rad[k], v_mul(st->thr[k], f3(mat.emission_color)));
+        st->thr[k] = v_mul(st->thr[k], f3(mat.diffuse_color));
+        float r1 = draw01(&rng), r2 = draw01(&rng);
+        st->rays[k].origin = pf3(v_add(min_point, bias));
+        st->rays[k].direction = pf3(hemisphere_cosine(mm, min_normal, r1, r2));
+    }
+    if (v_len(st->thr[k]) <= cfg->energy_exist_threshold) st->alive[ai] = -1;
+}
+
+/* thread_shrink: stable remove_if(v < 0) (parallel_function.cu:42-49) */
+static int shrink(int* a, int n) {
+    int w = 0;
+    for (int i = 0; i < n; i++)
+        if (a[i] >= 0) a[w++] = a[i];
+    return w;
+}
+
+/* pixel_256_transform_gamma_corrected (:627-682) for state slot k */
+static void gamma_u8(int mm, const pt_configuration* cfg, const float* img, int pass, unsigned char* out) {
+    or_v3 p = v_divs(v3(img[0], img[1], img[2]), (float)pass);
+    float c[3] = {p.x, p.y, p.z};
+    for (int i = 0; i < 3; i++) {
+        float x;
+        if (cfg->gamma_correction) x = or_clamp(m_exp(mm, 0.45454545f * m_log(mm, c[i])) * 255.0f, 0.0f, 255.0f);
+        else x = or_clamp(c[i] * 255.0f, 0.0f, 255.0f);
+        out[i] = (unsigned char)x;
+    }
+}
+
+/*
+ * Render passes first_pass .. first_pass+pass_count-1 for `n` pixels: pixel_list[k] (or k when
+ * pixel_list is NULL). image (n*3 floats) and image256 (n*3 bytes, may be NULL) are the running
+ * sum and 8-bit value of entry k, with the reference's pass_counter semantics. stats[0..2] (may be
+ * NULL) receive ray segments, BVH nodes visited and triangle tests. Returns 0 or -1 (alloc).
+ */
+int or_render(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangle* triangles, int sphere_num,
+              const pt_sphere* spheres, const pt_cube_map* cube, const pt_texture_wrapper* textures,
+              const pt_configuration* cfg, const pt_render_camera* cam, int first_pass, int pass_count,
+              const int* pixel_list, int n, float* image, unsigned char* image256, int rng_kind, int math_mode,
+              int threads, unsigned long long* stats) {
+    or_scene sc = {mesh_num, bvh_nodes, triangles, sphere_num, spheres, cube, textures, cfg, math_mode};
+    or_state st;
+    st.alive = (int*)malloc((size_t)n * sizeof(int));
+    st.rays = (pt_ray*)malloc((size_t)n * sizeof(pt_ray));
+    st.thr = (or_v3*)malloc((size_t)n * sizeof(or_v3));
+    st.rad = (or_v3*)malloc((size_t)n * sizeof(or_v3));
+    st.sca = (pt_scattering*)malloc((size_t)n * sizeof(pt_scattering));
+    if (!st.alive || !st.rays || !st.thr || !st.rad || !st.sca) {
+        free(st.alive); free(st.rays); free(st.thr); free(st.rad); free(st.sca);
+        return -1;
+    }
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+    unsigned long long segs = 0, nodes = 0, tris = 0;
+    for (int pass = first_pass; pass < first_pass + pass_count; pass++) {
+        int seed = pass;
+        #pragma omp parallel for schedule(dynamic, 256)
+        for (int k = 0; k < n; k++) generate(&sc, cam, rng_kind, seed, k, pixel_list ? pixel_list[k] : k, &st);
+        int count = n;
+        for (int depth = 0; depth < cfg->max_tracer_depth; depth++) {
+            if (count == 0) break;
+            segs += (unsigned long long)count;
+            unsigned long long dn = 0, dt = 0;
+            #pragma omp parallel for schedule(dynamic, 256) reduction(+ : dn, dt)
+            for (int ai = 0; ai < count; ai++) {
+                or_counts c = {0, 0};
+                trace(&sc, rng_kind, seed, depth, pixel_list, ai, &st, &c);
+                dn += c.nodes;
+                dt += c.tris;
+            }
+            nodes += dn;
+            tris += dt;
+            count = shrink(st.alive, count);
+        }
+        float hi = (float)cfg->max_tracer_depth * 2.0f;
+        #pragma omp parallel for schedule(static)
+        for (int k = 0; k < n; k++) {
+            float* img = image + (size_t)k * 3;
+            or_v3 c = v3(or_clamp(st.rad[k].x, 0.0f, hi), or_clamp(st.rad[k].y, 0.0f, hi), or_clamp(st.rad[k].z, 0.0f, hi));
+            if (pass != 1) { img[0] = img[0] + c.x; img[1] = img[1] + c.y; img[2] = img[2] + c.z; }
+            else { img[0] = c.x; img[1] = c.y; img[2] = c.z; }
+            if (image256) gamma_u8(math_mode, cfg, img, pass, image256 + (size_t)k * 3);
+        }
+    }
+    if (stats) { stats[0] = segs; stats[1] = nodes; stats[2] = tris; }
+    free(st.alive); free(st.rays); free(st.thr); free(st.rad); free(st.sca);
+    return 0;
+}
+
+/* Math known-answer exports (tests/test_oracle_math.py). */
+void or_math_eval(int which, int math_mode, const float* x, int n, float* out0, float* out1) {
+    for (int i = 0; i < n; i++) {
+        switch (which) {
+            case 0: m_sincos(math_mode, x[i], &out0[i], &out1[i]); break;
+            case 1: out0[i] = m_exp(math_mode, x[i]); break;
+            case 2: out0[i] = m_log(math_mode, x[i]); break;
+            case 3: out0[i] = m_atan(math_mode, x[i]); break;
+            case 4: out0[i] = m_asin(math_mode, x[i]); break;
+            case 5: out0[i] = m_acos(math_mode, x[i]); break;
+            case 6: out0[i] = m_pow(math_mode, x[i], 1.85f); break;
+            case 7: out0[i] = m_tan(math_mode, x[i]); break;
+            default: out0[i] = 0.0f;
+        }
+    }
+}

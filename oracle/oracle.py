@@ -1,0 +1,90 @@
+"""TEST INFRASTRUCTURE — Python binding of the C oracle (oracle/oracle.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module; the
+product package never does. The oracle takes the reference's own data layout (the SceneView of a
+pathtracerwithcuda_amd.Scene, i.e. the pointers a reference caller passes to path_tracer_kernel).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "lib", "liboracle.so")
+
+RNG = {"thrust": 0, "msvc": 1}
+MATH = {"cephes": 0, "libm": 1}
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    srcs = [os.path.join(HERE, f) for f in ("oracle.c", "oracle_math.h", "Makefile")]
+    if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
+        subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "lib/liboracle.so"], check=True)
+    return LIB
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        build()
+        h = C.CDLL(LIB)
+        h.or_render.restype = C.c_int
+        h.or_render.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                                C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        h.or_rng_stream.restype = None
+        h.or_rng_stream.argtypes = [C.c_int, C.c_int32, C.c_int, C.c_float, C.c_float, C.c_void_p]
+        h.or_hash.restype = C.c_int32
+        h.or_hash.argtypes = [C.c_int32]
+        h.or_math_eval.restype = None
+        h.or_math_eval.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        _lib = h
+    return _lib
+
+
+def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.ndarray | None = None,
+           rng: str = "thrust", math: str = "cephes", threads: int = 0, with_u8: bool = True):
+    """Run passes first_pass..first_pass+pass_count-1 over all pixels (or the given pixel indices).
+
+    Returns (image float32 [n,3], image256 uint8 [n,3] or None, stats dict)."""
+    L = lib()
+    if pixels is None:
+        n = int(cam.resolution[0]) * int(cam.resolution[1])
+        plist = None
+    else:
+        plist = np.ascontiguousarray(pixels, np.int32)
+        n = len(plist)
+    img = np.zeros((n, 3), np.float32)
+    img8 = np.zeros((n, 3), np.uint8) if with_u8 else None
+    stats = (C.c_ulonglong * 3)()
+    rc = L.or_render(view.mesh_num, C.cast(view.bvh_nodes, C.c_void_p), C.cast(view.triangles, C.c_void_p),
+                     view.sphere_num, C.cast(view.spheres, C.c_void_p), C.cast(view.sky_cube_map, C.c_void_p),
+                     C.cast(view.mesh_textures, C.c_void_p), C.addressof(cfg), C.addressof(cam), first_pass,
+                     pass_count, plist.ctypes.data if plist is not None else None, n, img.ctypes.data,
+                     img8.ctypes.data if img8 is not None else None, RNG[rng], MATH[math], threads, stats)
+    if rc != 0:
+        raise MemoryError("oracle allocation failed")
+    return img, img8, {"segments": stats[0], "nodes": stats[1], "tris": stats[2]}
+
+
+def rng_stream(kind: str, seed: int, n: int, a: float = 0.0, b: float = 1.0) -> np.ndarray:
+    out = np.empty(n, np.float32)
+    lib().or_rng_stream(RNG[kind], int(np.int32(seed)), n, a, b, out.ctypes.data)
+    return out
+
+
+def hash_(a: int) -> int:
+    return int(lib().or_hash(int(np.int32(a))))
+
+
+def math_eval(which: int, mode: str, x: np.ndarray):
+    x = np.ascontiguousarray(x, np.float32)
+    o0 = np.empty_like(x)
+    o1 = np.empty_like(x)
+    lib().or_math_eval(which, MATH[mode], x.ctypes.data, len(x), o0.ctypes.data, o1.ctypes.data)
+    return o0, o1

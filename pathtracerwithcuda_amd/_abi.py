@@ -1,0 +1,237 @@
+"""ctypes mirror of include/pt_types.h, include/pt_host.h, include/pt_native.h and
+include/path_tracer_kernel.h, plus the loader for libpt_hip.so.
+
+The library is the product: when it is missing or fails to load, every entry point raises — there
+is no CPU fallback anywhere in this package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from .build import LIB
+
+c_float_p = C.POINTER(C.c_float)
+c_int_p = C.POINTER(C.c_int)
+c_ubyte_p = C.POINTER(C.c_ubyte)
+
+
+class Float3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class Float2(C.Structure):
+    _pack_ = 8
+    _fields_ = [("x", C.c_float), ("y", C.c_float)]
+
+
+class UChar3(C.Structure):
+    _fields_ = [("x", C.c_ubyte), ("y", C.c_ubyte), ("z", C.c_ubyte)]
+
+
+class Ray(C.Structure):  # Core/ray.h:9-18
+    _fields_ = [("origin", Float3), ("direction", Float3)]
+
+
+class Scattering(C.Structure):  # Core/material.h:17-29
+    _fields_ = [("absorption_coefficient", Float3), ("reduced_scattering_coefficient", Float3)]
+
+
+class Medium(C.Structure):  # Core/material.h:31-47
+    _fields_ = [("refraction_index", C.c_float), ("extinction_coefficient", C.c_float), ("scattering", Scattering)]
+
+
+class Material(C.Structure):  # Core/material.h:49-78
+    _fields_ = [
+        ("diffuse_color", Float3),
+        ("emission_color", Float3),
+        ("specular_color", Float3),
+        ("is_transparent", C.c_ubyte),
+        ("roughness", C.c_float),
+        ("medium", Medium),
+        ("diffuse_texture_id", C.c_int),
+        ("specular_texture_id", C.c_int),
+    ]
+
+
+class Sphere(C.Structure):  # Core/sphere.h:11-16
+    _fields_ = [("center", Float3), ("radius", C.c_float), ("mat", Material)]
+
+
+class Triangle(C.Structure):  # Core/triangle.h:10-25
+    _fields_ = [
+        ("vertex0", Float3), ("vertex1", Float3), ("vertex2", Float3),
+        ("normal0", Float3), ("normal1", Float3), ("normal2", Float3),
+        ("uv0", C.c_float * 2), ("uv1", C.c_float * 2), ("uv2", C.c_float * 2),
+        ("mat", C.POINTER(Material)),
+    ]
+
+
+class BoundingBox(C.Structure):  # Bvh/bounding_box.h:7-10
+    _fields_ = [("left_bottom", Float3), ("right_top", Float3), ("centroid", Float3)]
+
+
+class BvhNodeDevice(C.Structure):  # Bvh/bvh_node.h:41-47
+    _fields_ = [
+        ("box", BoundingBox),
+        ("_pad", C.c_uint32),
+        ("triangle_indices", c_int_p),
+        ("is_leaf", C.c_ubyte),
+        ("next_node_index", C.c_int),
+    ]
+
+
+class RenderCamera(C.Structure):  # Core/camera.h:14-23
+    _fields_ = [
+        ("eye", Float3), ("view", Float3), ("up", Float3), ("_pad", C.c_uint32),
+        ("resolution", C.c_float * 2), ("fov", C.c_float * 2),
+        ("aperture_radius", C.c_float), ("focal_distance", C.c_float),
+    ]
+
+
+class Configuration(C.Structure):  # Core/configuration.h:9-34
+    _fields_ = [
+        ("width", C.c_int), ("height", C.c_int), ("use_fullscreen", C.c_ubyte),
+        ("block_size", C.c_int), ("max_block_size", C.c_int), ("max_tracer_depth", C.c_int),
+        ("vector_bias_length", C.c_float), ("energy_exist_threshold", C.c_float), ("sss_threshold", C.c_float),
+        ("use_sky_box", C.c_ubyte), ("use_sky", C.c_ubyte), ("use_bilinear", C.c_ubyte),
+        ("gamma_correction", C.c_ubyte), ("use_anti_alias", C.c_ubyte),
+        ("fov", C.c_float), ("bvh_leaf_node_triangle_num", C.c_int), ("bvh_bucket_max_divide_internal_num", C.c_int),
+        ("bvh_build_block_size", C.c_int), ("bvh_build", C.c_int), ("air_refraction_index", C.c_float),
+        ("air_absorption_coef", Float3), ("air_reduced_scattering_coef", Float3), ("cuda_acceleration", C.c_ubyte),
+    ]
+
+
+class CubeMap(C.Structure):  # Core/cube_map.h:9-18
+    _fields_ = [
+        ("m_x_positive_map", c_ubyte_p), ("m_x_negative_map", c_ubyte_p),
+        ("m_y_positive_map", c_ubyte_p), ("m_y_negative_map", c_ubyte_p),
+        ("m_z_positive_map", c_ubyte_p), ("m_z_negative_map", c_ubyte_p),
+        ("length", C.c_int),
+    ]
+
+
+class TextureWrapper(C.Structure):  # Core/texture.h:9-13
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("pixels", c_ubyte_p)]
+
+
+class SceneView(C.Structure):  # include/pt_host.h
+    _fields_ = [
+        ("mesh_num", C.c_int),
+        ("bvh_nodes", C.POINTER(C.POINTER(BvhNodeDevice))),
+        ("triangles", C.POINTER(Triangle)),
+        ("triangle_num", C.c_int),
+        ("sphere_num", C.c_int),
+        ("spheres", C.POINTER(Sphere)),
+        ("sky_cube_map", C.POINTER(CubeMap)),
+        ("mesh_textures", C.POINTER(TextureWrapper)),
+        ("texture_num", C.c_int),
+        ("materials", C.POINTER(Material)),
+        ("material_num", C.c_int),
+        ("mesh_node_num", c_int_p),
+        ("mesh_triangle_start", c_int_p),
+        ("mesh_triangle_num", c_int_p),
+    ]
+
+
+class ViewCamera(C.Structure):  # include/pt_host.h (Core/camera.h:27-80)
+    _fields_ = [
+        ("center", Float3), ("yaw", C.c_float), ("pitch", C.c_float), ("radius", C.c_float),
+        ("aperture_radius", C.c_float), ("focal_distance", C.c_float),
+        ("resolution", C.c_float * 2), ("fov", C.c_float * 2),
+    ]
+
+
+LAYOUT = {  # include/pt_types.h static asserts
+    "Ray": 24, "Scattering": 24, "Medium": 32, "Material": 84, "Sphere": 100, "Triangle": 104,
+    "BoundingBox": 36, "BvhNodeDevice": 56, "RenderCamera": 64, "Configuration": 96, "CubeMap": 56,
+    "TextureWrapper": 16,
+}
+
+# name -> (restype, argtypes)
+_PROTOS = {
+    # reference ABI (include/path_tracer_kernel.h)
+    "path_tracer_kernel": (None, [C.c_int, C.POINTER(C.POINTER(BvhNodeDevice)), C.POINTER(Triangle), C.c_int,
+                                  C.POINTER(Sphere), C.c_int, C.POINTER(Float3), C.POINTER(UChar3), C.c_int,
+                                  C.POINTER(RenderCamera), C.POINTER(CubeMap), C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.POINTER(TextureWrapper), C.POINTER(Configuration)]),
+    "path_tracer_kernel_memory_allocate": (None, [C.POINTER(C.c_void_p)] * 5 + [C.c_int]),
+    "path_tracer_kernel_memory_free": (None, [C.c_void_p] * 5),
+    "thread_shrink": (C.c_int, [C.c_void_p, C.c_int]),
+    # native (include/pt_native.h)
+    "pt_last_error": (C.c_char_p, []),
+    "pt_device_count": (C.c_int, []),
+    "pt_context_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "pt_context_destroy": (None, [C.c_void_p]),
+    "pt_scene_upload": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.POINTER(BvhNodeDevice)), C.POINTER(Triangle),
+                                  C.c_int, C.c_int, C.POINTER(Sphere), C.POINTER(CubeMap), C.POINTER(TextureWrapper),
+                                  C.c_int, C.POINTER(Configuration)]),
+    "pt_scene_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong), c_int_p, c_int_p]),
+    "pt_frame_setup": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "pt_set_tiling": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
+    "pt_render_passes": (C.c_int, [C.c_void_p, C.POINTER(RenderCamera), C.POINTER(Configuration), C.c_int, C.c_int,
+                                   C.c_int]),
+    "pt_finalize_u8": (C.c_int, [C.c_void_p, C.POINTER(Configuration), C.c_int]),
+    "pt_synchronize": (C.c_int, [C.c_void_p]),
+    "pt_image_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "pt_image_device_ptr": (C.c_void_p, [C.c_void_p]),
+    "pt_image256_device_ptr": (C.c_void_p, [C.c_void_p]),
+    "pt_stats_reset": (C.c_int, [C.c_void_p]),
+    "pt_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
+    "pt_stats_all": (C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]),
+    "pt_set_instrumented":(C.c_int, [C.c_void_p, C.c_int]),
+    "pt_kernel_time": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), c_int_p]),
+    "pt_math_eval_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    # host (include/pt_host.h)
+    "pt_bvh_build": (C.c_int, [C.POINTER(Triangle), C.c_int, C.c_int, C.c_int, C.c_int,
+                               C.POINTER(C.POINTER(BvhNodeDevice)), c_int_p, C.POINTER(c_int_p), c_int_p]),
+    "pt_bvh_free": (None, [C.POINTER(BvhNodeDevice), c_int_p]),
+    "pt_morton_code": (C.c_uint, [C.c_float, C.c_float, C.c_float]),
+    "pt_clz_table": (C.c_uint, [C.c_uint]),
+    "pt_scene_builder_create": (C.c_void_p, []),
+    "pt_scene_builder_destroy": (None, [C.c_void_p]),
+    "pt_scene_builder_add_material": (C.c_int, [C.c_void_p, C.POINTER(Material)]),
+    "pt_scene_builder_add_sphere": (C.c_int, [C.c_void_p, Float3, C.c_float, C.POINTER(Material)]),
+    "pt_scene_builder_add_mesh": (C.c_int, [C.c_void_p, C.c_int, c_float_p, c_float_p, c_float_p, c_int_p, Float3,
+                                            Float3, Float3]),
+    "pt_scene_builder_set_cube_map": (C.c_int, [C.c_void_p, C.c_int, c_ubyte_p]),
+    "pt_scene_builder_add_texture": (C.c_int, [C.c_void_p, C.c_int, C.c_int, c_ubyte_p]),
+    "pt_scene_builder_build": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "pt_scene_builder_view": (C.c_int, [C.c_void_p, C.POINTER(SceneView)]),
+    "pt_view_camera_default": (None, [C.POINTER(ViewCamera)]),
+    "pt_view_camera_set_resolution": (None, [C.POINTER(ViewCamera), C.c_float, C.c_float]),
+    "pt_view_camera_set_fov": (None, [C.POINTER(ViewCamera), C.c_float]),
+    "pt_view_camera_get_render_camera": (None, [C.POINTER(ViewCamera), C.POINTER(RenderCamera)]),
+    "pt_configuration_default": (None, [C.POINTER(Configuration)]),
+}
+
+EXPORTED = tuple(_PROTOS)
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libpt_hip.so (building it first if it is absent and hipcc is available)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        from .build import build
+        build()
+    handle = C.CDLL(LIB, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(handle, name)  # AttributeError = missing export: fail loudly
+        fn.restype = res
+        fn.argtypes = args
+    _lib = handle
+    return _lib
+
+
+class PtError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().pt_last_error()
+        raise PtError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

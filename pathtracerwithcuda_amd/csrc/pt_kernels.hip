@@ -1,0 +1,249 @@
+// pt_kernels.hip — HIP kernels of the radiance loop for gfx950.
+//
+// Reference structure (Kernel/path_tracer_kernel.cu:685-780): per pass, init_data_kernel ->
+// generate_ray_kernel -> max_depth x (trace_ray_kernel + thrust::remove_if compaction with a
+// host read-back of the live count) -> pixel_256_transform_gamma_corrected_kernel.
+//
+// Here one pass is ONE persistent launch. Each 64-lane wave owns up to 64 paths held entirely
+// in registers (the reference round-trips 76 B/pixel of path state through memory every depth).
+// A lane whose path terminates (killed, escaped, or max depth reached) writes its pixel's
+// running sum and 8-bit value and is refilled from a global pixel counter: the wave ballots the
+// lanes that need work, the first such lane takes popc(ballot) pixels with ONE atomicAdd, and
+// each lane takes its rank among them (mbcnt). That is the reference's thread_shrink compaction
+// (stable remove_if of dead pixels) done in-register, per wave, with no host synchronisation.
+// Results do not depend on the schedule: every random draw is seeded by (pass, pixel, depth)
+// (path_tracer_kernel.cu:324,415) and a pixel's passes are ordered by the launch sequence.
+#include "pt_kernels.h"
+
+namespace pt {
+
+template <bool LEAF1, bool STATS>
+__global__ __launch_bounds__(PT_BLOCK) void pass_kernel(DevScene sc, DevConfig cfg, DevCamera cam, DevTiling til,
+                                                        DevOutput out, int pass, int write_u8) {
+    const int lane = threadIdx.x & 63;
+    const int32_t hseed = hash_pt(pass);
+    const float clamp_hi = (float)cfg.max_depth * 2.0f;
+    const unsigned long long lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+    PathState ps;
+    int pixel = -1;
+    int depth = 0;
+    bool need = true;   // lane wants a new path
+    bool done = false;  // work counter exhausted for this lane
+    unsigned long long segments = 0;
+    Counters ctr = {0u, 0u, 0u, 0u, 0u, 0u};
+    unsigned long long csum[6] = {0, 0, 0, 0, 0, 0};
+
+    while (true) {
+        const bool want = need && !done;
+        const unsigned long long need_mask = __ballot(want);
+        if (need_mask) {
+            const int leader = __ffsll((long long)need_mask) - 1;
+            unsigned int base = 0;
+            if (lane == leader) base = atomicAdd(out.fetch, (unsigned int)__popcll(need_mask));
+            base = __shfl(base, leader);
+            if (want) {
+                const unsigned int u = base + (unsigned int)__popcll(need_mask & lane_lt);
+                need = false;
+                if (u < (unsigned int)til.unit_count) {
+                    if (til.band_count == 1) {
+                        pixel = (int)u;
+                    } else {
+                        int row_local = (int)u / til.width;
+                        int x = (int)u - row_local * til.width;
+                        int band_local = row_local / til.band_rows;
+                        int row_in_band = row_local - band_local * til.band_rows;
+                        int y = (band_local * til.band_count + til.band_index) * til.band_rows + row_in_band;
+                        pixel = y * til.width + x;
+                    }
+                    generate_path(cam, cfg, pixel, hseed, &ps);
+                    depth = 0;
+                } else {
+                    done = true;
+                }
+            }
+        }
+        if (!__any(!done)) break;
+        if (!done) {
+            bool alive = false;
+            if (depth < cfg.max_depth) {
+                alive = trace_step<LEAF1, STATS>(sc, cfg, pixel, depth, hseed, &ps, &ctr);
+                depth++;
+                segments++;
+                if (STATS) {
+                    csum[0] += ctr.nodes; csum[1] += ctr.tris; csum[2] += ctr.hit_mesh;
+                    csum[3] += ctr.hit_sphere; csum[4] += ctr.miss; csum[5] += ctr.scatter;
+                    ctr = Counters{0u, 0u, 0u, 0u, 0u, 0u};
+                }
+            }
+            if (!alive || depth >= cfg.max_depth) {
+                // pixel_256_transform_gamma_corrected_kernel (:644-680) for this pixel
+                float* img = out.image + (size_t)pixel * 3;
+                v3 c = clamp3(ps.rad, 0.0f, clamp_hi);
+                v3 sum;
+                if (pass != 1) sum = mk3(img[0], img[1], img[2]) + c;
+                else sum = c;
+                img[0] = sum.x; img[1] = sum.y; img[2] = sum.z;
+                if (write_u8 && out.image256) store_u8(cfg, sum, pass, out.image256 + (size_t)pixel * 3);
+                need = true;
+            }
+        }
+    }
+
+    // ray-segment count = sum of the live counts thread_shrink would return (metric numerator)
+    unsigned long long s = segments;
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (STATS) {
+#pragma unroll
+        for (int k = 0; k < 6; k++)
+            for (int off = 32; off > 0; off >>= 1) csum[k] += __shfl_xor(csum[k], off);
+    }
+    if (lane == 0) {
+        atomicAdd(&out.stats[0], s);
+        if (STATS) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) atomicAdd(&out.stats[1 + k], csum[k]);
+        }
+    }
+}
+
+// Gamma/8-bit from a float running sum (used after a multi-GPU reduce, and by the reference
+// ABI when the caller asks for the 8-bit image only at the end of a frame).
+__global__ __launch_bounds__(PT_BLOCK) void u8_kernel(DevConfig cfg, const float* image, uint8_t* image256,
+                                                      int pixel_count, int pass) {
+    int i = blockIdx.x * PT_BLOCK + threadIdx.x;
+    if (i >= pixel_count) return;
+    const float* p = image + (size_t)i * 3;
+    store_u8(cfg, mk3(p[0], p[1], p[2]), pass, image256 + (size_t)i * 3);
+}
+
+// Diagnostic: the device transcendentals on an array (bitwise check against the oracle's).
+__global__ __launch_bounds__(PT_BLOCK) void math_eval_kernel(int which, const float* x, int n, float* o0, float* o1) {
+    int i = blockIdx.x * PT_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    float a = x[i], r0 = 0.0f, r1 = 0.0f;
+    switch (which) {
+        case 0: sincos_pt(a, &r0, &r1); break;
+        case 1: r0 = exp_pt(a); break;
+        case 2: r0 = log_pt(a); break;
+        case 3: r0 = atan_pt(a); break;
+        case 4: r0 = asin_pt(a); break;
+        case 5: r0 = acos_pt(a); break;
+        case 6: r0 = pow_pt(a, 1.85f); break;
+        case 7: r0 = tan_pt(a); break;
+        case 8: r0 = sqrtf(a); r1 = 1.0f / a; break;
+        default: break;
+    }
+    o0[i] = r0;
+    o1[i] = r1;
+}
+
+hipError_t launch_math_eval(int which, const float* x, int n, float* o0, float* o1, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(math_eval_kernel, dim3((n + PT_BLOCK - 1) / PT_BLOCK), dim3(PT_BLOCK), 0, stream, which, x, n,
+                       o0, o1);
+    return hipGetLastError();
+}
+
+// ---- thread_shrink (Kernel/parallel_function.cu:42-49): stable remove_if(v < 0) -----------
+// Three passes over 256-element tiles: per-tile survivor counts (wave ballots), an exclusive
+// scan of the tile counts in one workgroup, then a stable scatter into a scratch array.
+__global__ __launch_bounds__(256) void shrink_count_kernel(const int* in, int n, int* tile_counts) {
+    __shared__ int wave_cnt[4];
+    int i = blockIdx.x * 256 + threadIdx.x;
+    bool keep = i < n && in[i] >= 0;
+    unsigned long long m = __ballot(keep);
+    if ((threadIdx.x & 63) == 0) wave_cnt[threadIdx.x >> 6] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) tile_counts[blockIdx.x] = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+}
+
+__global__ __launch_bounds__(1024) void shrink_scan_kernel(int* tile_counts, int tiles, int* total) {
+    __shared__ int part[1024];
+    // each thread scans a contiguous chunk, then the chunk sums are scanned in LDS
+    int per = (tiles + 1023) / 1024;
+    int begin = threadIdx.x * per;
+    int end = min(begin + per, tiles);
+    int s = 0;
+    for (int i = begin; i < end; i++) s += tile_counts[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        int v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int run = part[threadIdx.x] - s;  // exclusive prefix of this chunk
+    for (int i = begin; i < end; i++) {
+        int c = tile_counts[i];
+        tile_counts[i] = run;
+        run += c;
+    }
+    if (threadIdx.x == 1023) *total = part[1023];
+}
+
+__global__ __launch_bounds__(256) void shrink_scatter_kernel(const int* in, int n, const int* tile_offsets, int* out) {
+    __shared__ int wave_cnt[4];
+    int i = blockIdx.x * 256 + threadIdx.x;
+    int v = i < n ? in[i] : -1;
+    bool keep = i < n && v >= 0;
+    unsigned long long m = __ballot(keep);
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) wave_cnt[w] = __popcll(m);
+    __syncthreads();
+    int base = tile_offsets[blockIdx.x];
+    for (int k = 0; k < w; k++) base += wave_cnt[k];
+    unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    if (keep) out[base + __popcll(m & lt)] = v;
+}
+
+// ---- host-side launchers ------------------------------------------------------------------
+hipError_t launch_pass(const DevScene& sc, const DevConfig& cfg, const DevCamera& cam, const DevTiling& til,
+                       const DevOutput& out, int pass, int write_u8, int grid, bool stats, hipStream_t stream) {
+    const bool leaf1 = sc.leaf_size == 1;
+    if (leaf1 && !stats) hipLaunchKernelGGL((pass_kernel<true, false>), dim3(grid), dim3(PT_BLOCK), 0, stream, sc, cfg, cam, til, out, pass, write_u8);
+    else if (leaf1 && stats) hipLaunchKernelGGL((pass_kernel<true, true>), dim3(grid), dim3(PT_BLOCK), 0, stream, sc, cfg, cam, til, out, pass, write_u8);
+    else if (!leaf1 && !stats) hipLaunchKernelGGL((pass_kernel<false, false>), dim3(grid), dim3(PT_BLOCK), 0, stream, sc, cfg, cam, til, out, pass, write_u8);
+    else hipLaunchKernelGGL((pass_kernel<false, true>), dim3(grid), dim3(PT_BLOCK), 0, stream, sc, cfg, cam, til, out, pass, write_u8);
+    return hipGetLastError();
+}
+
+hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256, int pixel_count, int pass,
+                     hipStream_t stream) {
+    if (pixel_count <= 0) return hipSuccess;
+    int grid = (pixel_count + PT_BLOCK - 1) / PT_BLOCK;
+    hipLaunchKernelGGL(u8_kernel, dim3(grid), dim3(PT_BLOCK), 0, stream, cfg, image, image256, pixel_count, pass);
+    return hipGetLastError();
+}
+
+int pass_grid_size(bool leaf1, bool stats) {
+    int dev = 0, cus = 0, blocks = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const void* fn = leaf1 ? (stats ? (const void*)pass_kernel<true, true> : (const void*)pass_kernel<true, false>)
+                           : (stats ? (const void*)pass_kernel<false, true> : (const void*)pass_kernel<false, false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, PT_BLOCK, 0) != hipSuccess || blocks <= 0) blocks = 4;
+    if (cus <= 0) cus = 256;
+    return cus * blocks;
+}
+
+hipError_t shrink(int* data, int n, int* scratch, int* tile_counts, int* total_dev, int* total_host, hipStream_t stream) {
+    if (n <= 0) { *total_host = 0; return hipSuccess; }
+    int tiles = (n + 255) / 256;
+    hipLaunchKernelGGL(shrink_count_kernel, dim3(tiles), dim3(256), 0, stream, data, n, tile_counts);
+    hipLaunchKernelGGL(shrink_scan_kernel, dim3(1), dim3(1024), 0, stream, tile_counts, tiles, total_dev);
+    hipLaunchKernelGGL(shrink_scatter_kernel, dim3(tiles), dim3(256), 0, stream, data, n, tile_counts, scratch);
+    hipError_t e = hipMemcpyAsync(total_host, total_dev, sizeof(int), hipMemcpyDeviceToHost, stream);
+    if (e != hipSuccess) return e;
+    e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return e;
+    if (*total_host > 0) {
+        e = hipMemcpyAsync(data, scratch, (size_t)*total_host * sizeof(int), hipMemcpyDeviceToDevice, stream);
+        if (e != hipSuccess) return e;
+        e = hipStreamSynchronize(stream);
+    }
+    return e;
+}
+
+}  // namespace pt

@@ -1,0 +1,502 @@
+// pt_path.h — per-ray device functions of the radiance loop.
+//
+// Each function restates one reference function (file:line given); the operation order of
+// every float expression follows the reference source so that, with contraction off, the
+// result is reproducible on the host (oracle/) bit-for-bit.
+#pragma once
+
+#include "pt_math.h"
+#include "pt_scene.h"
+
+namespace pt {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PT_LDG(p) __builtin_nontemporal_load(p)
+#endif
+
+__device__ __forceinline__ v3 f4xyz(float4 a) { return mk3(a.x, a.y, a.z); }
+__device__ __forceinline__ int f2i(float f) { return __float_as_int(f); }
+
+// path_tracer_kernel.cu:46-52
+__device__ __forceinline__ v3 reflection(v3 n, v3 in) {
+    return in - 2.0f * dot(n, in) * n;
+}
+
+// path_tracer_kernel.cu:54-83
+__device__ __forceinline__ v3 refraction(v3 n, v3 in, float in_n, float out_n) {
+    v3 i = in * -1.0f;
+    float ndi = dot(n, i);
+    float ratio = in_n / out_n;
+    float a = ratio * ndi;
+    float b = 1.0f - ratio * ratio * (1.0f - ndi * ndi);
+    if (b < 0.0f) return mk3(0.0f, 0.0f, 0.0f);
+    if (ndi > 0) return n * (a - sqrtf(b)) - ratio * i;
+    return n * (a + sqrtf(b)) - ratio * i;
+}
+
+// Orthonormal frame of sample_on_hemisphere_* (path_tracer_kernel.cu:175-189). The reference
+// leaves any_direction uninitialised when no component is below 1/sqrt(3); that cannot happen
+// for |n| <= 1, and (0,0,1) keeps the impossible case defined.
+__device__ __forceinline__ void tangent_frame(v3 n, v3* vi, v3* vj) {
+    v3 any;
+    if (fabsf(n.x) < kSQRT_ONE_THIRD) any = mk3(1.0f, 0.0f, 0.0f);
+    else if (fabsf(n.y) < kSQRT_ONE_THIRD) any = mk3(0.0f, 1.0f, 0.0f);
+    else any = mk3(0.0f, 0.0f, 1.0f);
+    *vi = normalize(cross(n, any));
+    *vj = cross(n, *vi);
+}
+
+// path_tracer_kernel.cu:163-192
+__device__ __forceinline__ v3 sample_cosine(v3 n, float r1, float r2) {
+    float cos_theta = sqrtf(r1);
+    float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+    float phi = r2 * kTWO_PI;
+    v3 vi, vj;
+    tangent_frame(n, &vi, &vj);
+    float sp, cp;
+    sincos_pt(phi, &sp, &cp);
+    return cos_theta * n + cp * sin_theta * vi + sp * sin_theta * vj;
+}
+
+// path_tracer_kernel.cu:194-223
+__device__ __forceinline__ v3 sample_ggx(v3 n, float roughness, float r1, float r2) {
+    float theta = atan_pt(roughness * sqrtf(r1) / sqrtf(1.0f - r1));
+    float phi = r2 * kTWO_PI;
+    float sin_theta, cos_theta;
+    sincos_pt(theta, &sin_theta, &cos_theta);
+    v3 vi, vj;
+    tangent_frame(n, &vi, &vj);
+    float sp, cp;
+    sincos_pt(phi, &sp, &cp);
+    return cos_theta * n + cp * sin_theta * vi + sp * sin_theta * vj;
+}
+
+// path_tracer_kernel.cu:225-236
+__device__ __forceinline__ v3 sample_sphere(float r1, float r2) {
+    float cos_theta = r1 * 2.0f - 1.0f;
+    float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+    float phi = r2 * kTWO_PI;
+    float sp, cp;
+    sincos_pt(phi, &sp, &cp);
+    return mk3(cos_theta, cp * sin_theta, sp * sin_theta);
+}
+
+// path_tracer_kernel.cu:238-249 (__powf(E, -a*d) -> exp)
+__device__ __forceinline__ v3 absorption(const float a[3], float d) {
+    return mk3(exp_pt(-1.0f * a[0] * d), exp_pt(-1.0f * a[1] * d), exp_pt(-1.0f * a[2] * d));
+}
+
+// path_tracer_kernel.cu:251-273
+__device__ __forceinline__ float ggx_g1(float roughness, v3 macro, v3 micro, v3 dir) {
+    v3 v = -1.0f * dir;
+    float vdn = dot(v, macro);
+    float vdm = dot(v, micro);
+    float positive = (vdm / vdn) > 0.0f ? 1.0f : 0.0f;
+    if (positive == 0.0f) return 0.0f;
+    float r2 = roughness * roughness;
+    float c2 = vdn * vdn;
+    float t2 = (1.0f - c2) / c2;
+    return 2.0f / (1.0f + sqrtf(1.0f + r2 * t2));
+}
+
+// Core/fresnel.h:11-49 (pow(x, 2.0f) -> x*x)
+__device__ __forceinline__ float fresnel_dielectric(v3 n, v3 in, float in_n, float out_n, v3 refr) {
+    float cos_in = dot(n, in * -1.0f);
+    float cos_out = dot(-1.0f * n, refr);
+    if (in_n > out_n && acos_pt(cos_in) >= asin_pt(out_n / in_n)) return 1.0f;
+    if (length(refr) <= 0.000005f || cos_out < 0) return 1.0f;
+    float s = (in_n * cos_in - out_n * cos_out) / (in_n * cos_in + out_n * cos_out);
+    float p = (in_n * cos_out - out_n * cos_in) / (in_n * cos_out + out_n * cos_in);
+    float rs = s * s;
+    float rp = p * p;
+    return (rs + rp) / 2.0f;
+}
+
+// Core/fresnel.h:51-76
+__device__ __forceinline__ float fresnel_conductor(v3 n, v3 in, float eta, float k) {
+    float cos_in = dot(n, in * -1.0f);
+    float n2 = eta * eta;
+    float k2 = k * k;
+    float nk = n2 + k2;
+    float c2 = cos_in * cos_in;
+    float two_n_c = 2 * eta * cos_in;
+    float rs = (nk * c2 - two_n_c + 1.0f) / (nk * c2 + two_n_c + 1.0f);
+    float rp = (nk - two_n_c + c2) / (nk + two_n_c + c2);
+    return (rs + rp) / 2.0f;
+}
+
+__device__ __forceinline__ v3 texel(const uint8_t* px, int idx) {
+    uchar4 c = *reinterpret_cast<const uchar4*>(px + (size_t)idx * 4);
+    return mk3((int)c.x / 255.0f, (int)c.y / 255.0f, (int)c.z / 255.0f);
+}
+
+// Core/texture.h:15-79 (also the face lookup of Core/cube_map.h:20-119, same arithmetic)
+__device__ __forceinline__ v3 sample_rgba8(const uint8_t* px, int w, int h, float au, float av, int bilinear) {
+    if (bilinear) {
+        float xr = au * (float)(w - 1);
+        float yr = (1.0f - av) * (float)(h - 1);
+        int fx = (int)clampf(floorf(xr), 0.0f, (float)(w - 1));
+        int cx = (int)clampf(ceilf(xr), 0.0f, (float)(w - 1));
+        int fy = (int)clampf(floorf(yr), 0.0f, (float)(h - 1));
+        int cy = (int)clampf(ceilf(yr), 0.0f, (float)(h - 1));
+        float lr = xr - floorf(xr);
+        float bt = yr - floorf(yr);
+        v3 c0 = texel(px, fy * w + fx);
+        v3 c1 = texel(px, fy * w + cx);
+        v3 c2 = texel(px, cy * w + fx);
+        v3 c3 = texel(px, cy * w + cx);
+        return lerp(lerp(c0, c1, lr), lerp(c2, c3, lr), bt);
+    }
+    int x = (int)clampf(au * (float)(w - 1), 0.0f, (float)(w - 1));
+    int y = (int)clampf((1.0f - av) * (float)(h - 1), 0.0f, (float)(h - 1));
+    return texel(px, y * w + x);
+}
+
+__device__ __forceinline__ v3 sample_texture(const DevScene& sc, int id, v2 uv, int bilinear) {
+    int4 d = sc.tex_desc[id];
+    float au = uv.x - floorf(uv.x);
+    float av = uv.y - floorf(uv.y);
+    return sample_rgba8(sc.tex_pool + (size_t)(unsigned)d.z, d.x, d.y, au, av, bilinear);
+}
+
+// Core/cube_map.h:20-119
+__device__ __forceinline__ v3 background(const DevScene& sc, const DevConfig& cfg, v3 d) {
+    if (cfg.use_sky_box) {
+        if (sc.cube_len <= 0) return mk3(0.0f, 0.0f, 0.0f);
+        float u, v;
+        int face;
+        xyz_to_cube_uv(d.x, d.y, d.z, &face, &u, &v);
+        int len = sc.cube_len;
+        const uint8_t* px = sc.cube + (size_t)face * (size_t)len * (size_t)len * 4;
+        return sample_rgba8(px, len, len, u, v, cfg.use_bilinear);
+    }
+    if (cfg.use_sky) {
+        float t = (dot(d, mk3(-0.41f, 0.41f, -0.82f)) + 1.0f) / 2.0f;
+        v3 a = mk3(0.15f, 0.3f, 0.5f);
+        v3 b = mk3(1.0f, 1.0f, 1.0f);
+        return ((1.0f - t) * a + t * b) * 1.0f;
+    }
+    return mk3(0.0f, 0.0f, 0.0f);
+}
+
+// Core/sphere.h:18-55 -> t only; the hit point/normal are derived for the winner afterwards.
+__device__ __forceinline__ bool sphere_t(float4 s, v3 o, v3 d, float* t_out) {
+    v3 op = mk3(s.x, s.y, s.z) - o;
+    float b = dot(op, d);
+    float delta = b * b - dot(op, op) + s.w * s.w;
+    if (delta < 0) return false;
+    float dr = sqrtf(delta);
+    float t1 = b - dr;
+    float t2 = b + dr;
+    if (t1 < 0 && t2 < 0) return false;
+    *t_out = (t1 > 0 && t2 > 0) ? fminf(t1, t2) : fmaxf(t1, t2);
+    return true;
+}
+
+// Core/triangle.h:27-62 with edge1/edge2 precomputed (same IEEE subtraction, done once).
+__device__ __forceinline__ bool triangle_t(const float4* tg, int tri, v3 o, v3 d,
+                                           float* t, float* t1o, float* t2o) {
+    float4 a = tg[3 * tri + 0];
+    float4 b = tg[3 * tri + 1];
+    float4 c = tg[3 * tri + 2];
+    v3 v0 = f4xyz(a), e1 = f4xyz(b), e2 = f4xyz(c);
+    v3 p = cross(d, e2);
+    float det = dot(e1, p);
+    if (det == 0.0f) return false;
+    float inv = 1.0f / det;
+    v3 tv = o - v0;
+    v3 q = cross(tv, e1);
+    float t1 = dot(tv, p) * inv;
+    float t2 = dot(d, q) * inv;
+    float tt = dot(e2, q) * inv;
+    if (t1 >= 0.0f && t2 >= 0.0f && t1 + t2 <= 1.0f) {
+        *t = tt; *t1o = t1; *t2o = t2;
+        return true;
+    }
+    return false;
+}
+
+// Bvh/bounding_box.h:83-102 with 1/direction hoisted out of the node loop.
+__device__ __forceinline__ bool box_hit(float4 lo, float4 hi, v3 o, v3 inv, float* entry) {
+    float tx1 = (lo.x - o.x) * inv.x;
+    float tx2 = (hi.x - o.x) * inv.x;
+    float ty1 = (lo.y - o.y) * inv.y;
+    float ty2 = (hi.y - o.y) * inv.y;
+    float tz1 = (lo.z - o.z) * inv.z;
+    float tz2 = (hi.z - o.z) * inv.z;
+    float t_max = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    float t_min = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    *entry = t_max;
+    return t_max <= t_min && t_min > 0.0f;
+}
+
+// Instrumentation (STATS kernels only): what one trace step touched, for the roofline model.
+struct Counters {
+    unsigned int nodes;       // BVH nodes fetched
+    unsigned int tris;        // triangle tests
+    unsigned int hit_mesh;    // closest hit on a triangle (shading reads normals/uvs/material)
+    unsigned int hit_sphere;  // closest hit on a sphere
+    unsigned int miss;        // escaped: background lookup
+    unsigned int scatter;     // subsurface free-flight event (no surface shading)
+};
+
+// path_tracer_kernel.cu:85-161: stackless preorder walk with skip indices over one mesh.
+template <bool LEAF1, bool STATS>
+__device__ __forceinline__ bool mesh_closest(const DevScene& sc, int begin, int end, v3 o, v3 d, v3 inv,
+                                             float* ht, float* ht1, float* ht2, int* htri, Counters* ctr) {
+    float min_t = __builtin_inff();
+    float min_t1 = 0.0f, min_t2 = 0.0f;
+    int min_tri = -1;
+    bool hit = false;
+    int pos = begin;
+    while (pos != end) {
+        float4 lo = sc.nodes[2 * pos + 0];
+        float4 hi = sc.nodes[2 * pos + 1];
+        if (STATS) ctr->nodes++;
+        float entry;
+        if (box_hit(lo, hi, o, inv, &entry) && entry <= min_t) {
+            int slot = f2i(hi.w);
+            if (slot >= 0) {
+                if (LEAF1) {
+                    float t, t1, t2;
+                    if (STATS) ctr->tris++;
+                    if (triangle_t(sc.tri_geom, slot, o, d, &t, &t1, &t2) && t > 0.0f && t < min_t) {
+                        min_t = t; min_t1 = t1; min_t2 = t2; min_tri = slot; hit = true;
+                    }
+                } else {
+                    for (int i = 0; i < sc.leaf_size; i++) {
+                        int tri = sc.leaf_tris[slot + i];
+                        if (tri == -1) break;
+                        float t, t1, t2;
+                        if (STATS) ctr->tris++;
+                        if (triangle_t(sc.tri_geom, tri, o, d, &t, &t1, &t2) && t > 0.0f && t < min_t) {
+                            min_t = t; min_t1 = t1; min_t2 = t2; min_tri = tri; hit = true;
+                        }
+                    }
+                }
+            }
+            pos++;
+        } else {
+            pos = f2i(lo.w);
+        }
+    }
+    if (hit) { *ht = min_t; *ht1 = min_t1; *ht2 = min_t2; *htri = min_tri; }
+    return hit;
+}
+
+// Per-path registers (the reference keeps these per pixel in HBM: rays, not_absorbed_colors,
+// accumulated_colors, scatterings; path_tracer_kernel.cu:275-297).
+struct PathState {
+    v3 o, d;
+    v3 thr;
+    v3 rad;
+    float sa[3];
+    float ss[3];
+};
+
+// init_data_kernel + generate_ray_kernel for one pixel (path_tracer_kernel.cu:275-379).
+__device__ __forceinline__ void generate_path(const DevCamera& cam, const DevConfig& cfg, int pixel,
+                                              int32_t hseed, PathState* ps) {
+    ps->thr = mk3(1.0f, 1.0f, 1.0f);
+    ps->rad = mk3(0.0f, 0.0f, 0.0f);
+    ps->sa[0] = cfg.air_absorption[0]; ps->sa[1] = cfg.air_absorption[1]; ps->sa[2] = cfg.air_absorption[2];
+    ps->ss[0] = cfg.air_reduced_scattering[0]; ps->ss[1] = cfg.air_reduced_scattering[1];
+    ps->ss[2] = cfg.air_reduced_scattering[2];
+
+    int image_y = (int)((float)pixel / cam.res_x);
+    int image_x = (int)((float)pixel - ((float)image_y * cam.res_x));
+    minstd rng = minstd_seed(mul_wrap(mul_wrap(hseed, hseed), hash_pt(pixel)));
+    float jx = 0.0f, jy = 0.0f;
+    if (cfg.use_anti_alias) {
+        jx = minstd_uniform(&rng, -0.5f, 0.5f);
+        jy = minstd_uniform(&rng, -0.5f, 0.5f);
+    }
+    v3 eye = mk3(cam.eye[0], cam.eye[1], cam.eye[2]);
+    v3 view = mk3(cam.view[0], cam.view[1], cam.view[2]);
+    v3 xa = mk3(cam.x_axis[0], cam.x_axis[1], cam.x_axis[2]);
+    v3 ya = mk3(cam.y_axis[0], cam.y_axis[1], cam.y_axis[2]);
+    float nx = (((float)image_x + jx) / (cam.res_x - 1.0f)) * 2.0f - 1.0f;
+    float ny = (((float)image_y + jy) / (cam.res_y - 1.0f)) * 2.0f - 1.0f;
+    v3 canvas = eye + view + nx * xa + ny * ya;
+    v3 image_plane = eye + normalize(canvas - eye) * cam.focal;
+    v3 ap;
+    if (cam.aperture > 0.00001f) {
+        float r1 = minstd_uniform(&rng, -0.5f, 0.5f) + 0.5f;
+        float r2 = minstd_uniform(&rng, -0.5f, 0.5f) + 0.5f;
+        float angle = r1 * kTWO_PI;
+        float dist = cam.aperture * sqrtf(r2);
+        float sa, ca;
+        sincos_pt(angle, &sa, &ca);
+        float ax = ca * dist;
+        float ay = sa * dist;
+        v3 hz = mk3(cam.horizontal[0], cam.horizontal[1], cam.horizontal[2]);
+        v3 vt = mk3(cam.vertical[0], cam.vertical[1], cam.vertical[2]);
+        ap = eye + ax * hz + ay * vt;
+    } else {
+        ap = eye;
+    }
+    ps->o = ap;
+    ps->d = normalize(image_plane - ap);
+}
+
+// One invocation of trace_ray_kernel for one live ray (path_tracer_kernel.cu:381-625).
+// Returns false when the reference would write -1 into energy_exist_pixels.
+template <bool LEAF1, bool STATS>
+__device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& cfg, int pixel, int depth,
+                                           int32_t hseed, PathState* ps, Counters* ctr) {
+    const v3 o = ps->o, d = ps->d;
+    minstd rng = minstd_seed(mul_wrap(mul_wrap(hseed, hash_pt(pixel)), hash_pt(depth)));
+
+    float min_t = __builtin_inff();
+    float min_t1 = __builtin_inff(), min_t2 = __builtin_inff();
+    int type = 0;  // 0 none, 1 sphere, 2 triangle
+    int min_sphere = -1, min_tri = -1;
+
+    for (int i = 0; i < sc.sphere_num; i++) {
+        float t;
+        if (sphere_t(sc.spheres[2 * i], o, d, &t) && t < min_t && t > 0.0f) {
+            min_t = t; min_sphere = i; type = 1;
+        }
+    }
+    if (sc.mesh_num > 0) {
+        v3 inv = 1.0f / d;
+        for (int m = 0; m < sc.mesh_num; m++) {
+            int2 r = sc.mesh_range[m];
+            float t, t1, t2;
+            int tri;
+            if (mesh_closest<LEAF1, STATS>(sc, r.x, r.y, o, d, inv, &t, &t1, &t2, &tri, ctr) && t < min_t && t > 0.0f) {
+                min_t = t; min_t1 = t1; min_t2 = t2; min_tri = tri; type = 2;
+            }
+        }
+    }
+
+    // medium: absorption and subsurface scattering (:456-492)
+    if (ps->ss[0] > 0.0f || length(mk3(ps->sa[0], ps->sa[1], ps->sa[2])) > cfg.sss_threshold) {
+        float r = minstd_uniform(&rng, 0.0f, 1.0f);
+        float dist = -log_pt(r) / ps->ss[0];
+        if (dist < min_t) {
+            float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
+            float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
+            ps->o = o + d * dist;
+            ps->d = sample_sphere(r1, r2);
+            ps->thr = ps->thr * absorption(ps->sa, dist);
+            if (STATS) ctr->scatter++;
+            return length(ps->thr) > cfg.energy_threshold;
+        }
+        ps->thr = ps->thr * absorption(ps->sa, min_t);
+    }
+
+    if (STATS) { ctr->miss += type == 0; ctr->hit_sphere += type == 1; ctr->hit_mesh += type == 2; }
+    if (type == 0) {  // miss (:618-624)
+        v3 bg = background(sc, cfg, d);
+        ps->rad = ps->rad + ps->thr * bg;
+        return false;
+    }
+
+    DevMaterial mat;
+    v3 point, normal;
+    if (type == 1) {
+        float4 s = sc.spheres[2 * min_sphere];
+        int mid = f2i(sc.spheres[2 * min_sphere + 1].x);
+        mat = sc.materials[mid];
+        point = o + d * min_t;
+        normal = normalize(point - mk3(s.x, s.y, s.z));
+    } else {
+        float4 s0 = sc.tri_shade[4 * min_tri + 0];
+        float4 s1 = sc.tri_shade[4 * min_tri + 1];
+        float4 s2 = sc.tri_shade[4 * min_tri + 2];
+        float4 s3 = sc.tri_shade[4 * min_tri + 3];
+        mat = sc.materials[f2i(s3.w)];
+        point = o + d * min_t;
+        v3 n0 = mk3(s0.x, s0.y, s0.z), n1 = mk3(s0.w, s1.x, s1.y), n2 = mk3(s1.z, s1.w, s2.x);
+        float w = 1.0f - min_t1 - min_t2;
+        normal = n0 * w + n1 * min_t1 + n2 * min_t2;
+        if (mat.diffuse_texture_id != -1 || mat.specular_texture_id != -1) {
+            v2 uv0 = mk2(s2.y, s2.z), uv1 = mk2(s2.w, s3.x), uv2 = mk2(s3.y, s3.z);
+            v2 uv = uv0 * w + uv1 * min_t1 + uv2 * min_t2;
+            if (mat.diffuse_texture_id != -1) {
+                v3 tc = sample_texture(sc, mat.diffuse_texture_id, uv, cfg.use_bilinear);
+                mat.diffuse[0] = mat.diffuse[0] * tc.x;
+                mat.diffuse[1] = mat.diffuse[1] * tc.y;
+                mat.diffuse[2] = mat.diffuse[2] * tc.z;
+            }
+            if (mat.specular_texture_id != -1) {
+                v3 tc = sample_texture(sc, mat.specular_texture_id, uv, cfg.use_bilinear);
+                mat.specular[0] = mat.specular[0] * tc.x;
+                mat.specular[1] = mat.specular[1] * tc.y;
+                mat.specular[2] = mat.specular[2] * tc.z;
+            }
+        }
+    }
+
+    // media on either side of the surface (:529-547)
+    float in_n = cfg.air_n;
+    float out_n = mat.refraction_index;
+    bool transparent = mat.is_transparent != 0;
+    float out_sa[3] = {mat.absorption[0], mat.absorption[1], mat.absorption[2]};
+    float out_ss[3] = {mat.reduced_scattering[0], mat.reduced_scattering[1], mat.reduced_scattering[2]};
+    if (dot(d, normal) > 0) {
+        normal = normal * -1.0f;
+        if (transparent) {
+            float tn = in_n; in_n = out_n; out_n = tn;
+            for (int c = 0; c < 3; c++) {
+                out_sa[c] = cfg.air_absorption[c];
+                out_ss[c] = cfg.air_reduced_scattering[c];
+            }
+        }
+    }
+    v3 refr = refraction(normal, d, in_n, out_n);
+    v3 bias_v = cfg.bias * normal;
+
+    float R;
+    if (mat.extinction_coefficient == 0 || transparent) R = fresnel_dielectric(normal, d, in_n, out_n, refr);
+    else R = fresnel_conductor(normal, d, out_n, mat.extinction_coefficient);
+
+    float r = minstd_uniform(&rng, 0.0f, 1.0f);
+    if (r < R) {  // reflection (:565-584)
+        float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
+        float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
+        float rough = pow_pt(mat.roughness, 1.85f) * 0.238f;
+        v3 micro = sample_ggx(normal, rough, r1, r2);
+        v3 mr = reflection(micro, d);
+        float shadow = ggx_g1(rough, normal, micro, d) * ggx_g1(rough, normal, micro, mr);
+        ps->o = point + bias_v;
+        ps->d = mr;
+        ps->thr = ps->thr * (mk3(mat.specular[0], mat.specular[1], mat.specular[2]) * shadow);
+    } else if (transparent) {  // refraction (:585-596)
+        ps->o = point - bias_v;
+        ps->d = refr;
+        for (int c = 0; c < 3; c++) { ps->sa[c] = out_sa[c]; ps->ss[c] = out_ss[c]; }
+        float ratio = out_n / in_n;
+        ps->thr = ps->thr * (ratio * ratio);
+    } else {  // diffuse (:597-610)
+        ps->rad = ps->rad + ps->thr * mk3(mat.emission[0], mat.emission[1], mat.emission[2]);
+        ps->thr = ps->thr * mk3(mat.diffuse[0], mat.diffuse[1], mat.diffuse[2]);
+        float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
+        float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
+        ps->o = point + bias_v;
+        ps->d = sample_cosine(normal, r1, r2);
+    }
+    return length(ps->thr) > cfg.energy_threshold;
+}
+
+// pixel_256_transform_gamma_corrected_kernel (path_tracer_kernel.cu:627-682) for one pixel.
+__device__ __forceinline__ void store_u8(const DevConfig& cfg, v3 sum, int pass, uint8_t* out3) {
+    v3 p = sum / (float)pass;
+    float x, y, z;
+    if (cfg.gamma_correction) {
+        const float inv_gamma = 0.45454545f;
+        x = clampf(exp_pt(inv_gamma * log_pt(p.x)) * 255.0f, 0.0f, 255.0f);
+        y = clampf(exp_pt(inv_gamma * log_pt(p.y)) * 255.0f, 0.0f, 255.0f);
+        z = clampf(exp_pt(inv_gamma * log_pt(p.z)) * 255.0f, 0.0f, 255.0f);
+    } else {
+        x = clampf(p.x * 255.0f, 0.0f, 255.0f);
+        y = clampf(p.y * 255.0f, 0.0f, 255.0f);
+        z = clampf(p.z * 255.0f, 0.0f, 255.0f);
+    }
+    out3[0] = (uint8_t)x;
+    out3[1] = (uint8_t)y;
+    out3[2] = (uint8_t)z;
+}
+
+}  // namespace pt

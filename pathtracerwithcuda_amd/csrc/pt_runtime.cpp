@@ -1,0 +1,730 @@
+// pt_runtime.cpp — context, scene translation/upload, the reference C-ABI and the native C-ABI.
+//
+// Host-side replacement of Kernel/path_tracer_kernel.cu:685-811 and Kernel/parallel_function.cu:42-49.
+// The reference reads a managed `configuration` on the host each pass (:706), launches
+// 3 + max_depth kernels and synchronises with the host after every depth (:767). Here a pass is
+// one launch on a private HIP stream (pt_kernels.hip); the host never waits inside a frame.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/path_tracer_kernel.h"
+#include "../../include/pt_native.h"
+#include "pt_kernels.h"
+
+using namespace pt;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+void set_error(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+}
+
+#define PT_HIP(call)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (call);                                                                   \
+        if (e_ != hipSuccess) {                                                                   \
+            set_error("[Hip]Error %s in file %s line %d: %s", hipGetErrorName(e_), __FILE__,      \
+                      __LINE__, hipGetErrorString(e_));                                           \
+            return PT_E_HIP;                                                                      \
+        }                                                                                         \
+    } while (0)
+
+inline float4 mkf4(float x, float y, float z, float w) { float4 r; r.x = x; r.y = y; r.z = z; r.w = w; return r; }
+inline float i2f(int i) { float f; std::memcpy(&f, &i, 4); return f; }
+
+struct SceneStage {
+    std::vector<float4> nodes;
+    std::vector<int> leaf_tris;
+    std::vector<int2> mesh_range;
+    std::vector<float4> tri_geom, tri_shade, spheres;
+    std::vector<DevMaterial> mats;
+    std::vector<int4> tex_desc;
+    std::vector<uint8_t> tex_pool, cube;
+    int cube_len = 0;
+    int leaf_size = 1;
+};
+
+DevMaterial to_dev(const pt_material& m) {
+    DevMaterial d;
+    std::memset(&d, 0, sizeof(d));
+    d.diffuse[0] = m.diffuse_color.x; d.diffuse[1] = m.diffuse_color.y; d.diffuse[2] = m.diffuse_color.z;
+    d.emission[0] = m.emission_color.x; d.emission[1] = m.emission_color.y; d.emission[2] = m.emission_color.z;
+    d.specular[0] = m.specular_color.x; d.specular[1] = m.specular_color.y; d.specular[2] = m.specular_color.z;
+    d.roughness = m.roughness;
+    d.refraction_index = m.medium.refraction_index;
+    d.extinction_coefficient = m.medium.extinction_coefficient;
+    const pt_scattering& s = m.medium.scattering;
+    d.absorption[0] = s.absorption_coefficient.x; d.absorption[1] = s.absorption_coefficient.y;
+    d.absorption[2] = s.absorption_coefficient.z;
+    d.reduced_scattering[0] = s.reduced_scattering_coefficient.x;
+    d.reduced_scattering[1] = s.reduced_scattering_coefficient.y;
+    d.reduced_scattering[2] = s.reduced_scattering_coefficient.z;
+    d.is_transparent = m.is_transparent ? 1 : 0;
+    d.diffuse_texture_id = m.diffuse_texture_id;
+    d.specular_texture_id = m.specular_texture_id;
+    return d;
+}
+
+// Reference layout -> device layout (pt_scene.h). Reads every embedded pointer on the host.
+int translate_scene(SceneStage& st, int mesh_num, pt_bvh_node_device** bvh_nodes, pt_triangle* tris, int tri_num,
+                    int sphere_num, pt_sphere* spheres, pt_cube_map* cube, pt_texture_wrapper* textures, int tex_num,
+                    const pt_configuration* cfg) {
+    st = SceneStage();
+    st.leaf_size = cfg->bvh_leaf_node_triangle_num > 0 ? cfg->bvh_leaf_node_triangle_num : 1;
+    if (mesh_num < 0 || sphere_num < 0) { set_error("negative mesh/sphere count"); return PT_E_ARG; }
+    if (mesh_num > 0 && (!bvh_nodes || !tris)) { set_error("meshes without bvh/triangles"); return PT_E_ARG; }
+    if (sphere_num > 0 && !spheres) { set_error("spheres pointer is null"); return PT_E_ARG; }
+
+    int max_tri = -1;
+    for (int m = 0; m < mesh_num; m++) {
+        const pt_bvh_node_device* nodes = bvh_nodes[m];
+        if (!nodes) { set_error("mesh %d has no bvh", m); return PT_E_ARG; }
+        const int count = nodes[0].next_node_index;  // root.next == node count (bvh.cpp:302-305)
+        const int base = (int)(st.nodes.size() / 2);
+        st.mesh_range.push_back(int2{base, base + count});
+        for (int i = 0; i < count; i++) {
+            const pt_bvh_node_device& n = nodes[i];
+            int slot = -1;
+            if (n.is_leaf && n.triangle_indices) {
+                if (st.leaf_size == 1) {
+                    slot = n.triangle_indices[0];
+                    if (slot > max_tri) max_tri = slot;
+                } else {
+                    slot = (int)st.leaf_tris.size();
+                    for (int k = 0; k < st.leaf_size; k++) {
+                        int t = n.triangle_indices[k];
+                        st.leaf_tris.push_back(t);
+                        if (t > max_tri) max_tri = t;
+                    }
+                }
+            }
+            const pt_bounding_box& b = n.box;
+            st.nodes.push_back(mkf4(b.left_bottom.x, b.left_bottom.y, b.left_bottom.z, i2f(n.next_node_index + base)));
+            st.nodes.push_back(mkf4(b.right_top.x, b.right_top.y, b.right_top.z, i2f(slot)));
+        }
+    }
+    const int T = tri_num >= 0 ? tri_num : max_tri + 1;
+    if (max_tri >= T) { set_error("bvh references triangle %d >= triangle_num %d", max_tri, T); return PT_E_ARG; }
+
+    std::unordered_map<const pt_material*, int> mat_index;
+    int max_tex = -1;
+    auto add_mat = [&](const pt_material& m) {
+        st.mats.push_back(to_dev(m));
+        if (m.diffuse_texture_id > max_tex) max_tex = m.diffuse_texture_id;
+        if (m.specular_texture_id > max_tex) max_tex = m.specular_texture_id;
+        return (int)st.mats.size() - 1;
+    };
+    st.tri_geom.reserve((size_t)T * 3);
+    st.tri_shade.reserve((size_t)T * 4);
+    for (int t = 0; t < T; t++) {
+        const pt_triangle& tr = tris[t];
+        int mid;
+        if (!tr.mat) { set_error("triangle %d has no material", t); return PT_E_ARG; }
+        auto it = mat_index.find(tr.mat);
+        if (it == mat_index.end()) { mid = add_mat(*tr.mat); mat_index.emplace(tr.mat, mid); }
+        else mid = it->second;
+        // edge1 / edge2 of triangle::intersect (Core/triangle.h:34-35), same float subtraction
+        st.tri_geom.push_back(mkf4(tr.vertex0.x, tr.vertex0.y, tr.vertex0.z, 0.0f));
+        st.tri_geom.push_back(mkf4(tr.vertex1.x - tr.vertex0.x, tr.vertex1.y - tr.vertex0.y, tr.vertex1.z - tr.vertex0.z, 0.0f));
+        st.tri_geom.push_back(mkf4(tr.vertex2.x - tr.vertex0.x, tr.vertex2.y - tr.vertex0.y, tr.vertex2.z - tr.vertex0.z, 0.0f));
+        st.tri_shade.push_back(mkf4(tr.normal0.x, tr.normal0.y, tr.normal0.z, tr.normal1.x));
+        st.tri_shade.push_back(mkf4(tr.normal1.y, tr.normal1.z, tr.normal2.x, tr.normal2.y));
+        st.tri_shade.push_back(mkf4(tr.normal2.z, tr.uv0.x, tr.uv0.y, tr.uv1.x));
+        st.tri_shade.push_back(mkf4(tr.uv1.y, tr.uv2.x, tr.uv2.y, i2f(mid)));
+    }
+    for (int s = 0; s < sphere_num; s++) {
+        const pt_sphere& sp = spheres[s];
+        int mid = add_mat(sp.mat);
+        st.spheres.push_back(mkf4(sp.center.x, sp.center.y, sp.center.z, sp.radius));
+        st.spheres.push_back(mkf4(i2f(mid), 0.0f, 0.0f, 0.0f));
+    }
+    const int K = tex_num >= 0 ? tex_num : max_tex + 1;
+    if (max_tex >= K || (K > 0 && !textures)) { set_error("material texture id %d without texture data", max_tex); return PT_E_ARG; }
+    for (int k = 0; k < K; k++) {
+        const pt_texture_wrapper& tw = textures[k];
+        if (tw.width <= 0 || tw.height <= 0 || !tw.pixels) { set_error("texture %d is empty", k); return PT_E_ARG; }
+        st.tex_desc.push_back(int4{tw.width, tw.height, (int)st.tex_pool.size(), 0});
+        st.tex_pool.insert(st.tex_pool.end(), tw.pixels, tw.pixels + (size_t)tw.width * tw.height * 4);
+    }
+    if (cube && cube->length > 0) {
+        const unsigned char* faces[6] = {cube->m_x_positive_map, cube->m_x_negative_map, cube->m_y_positive_map,
+                                         cube->m_y_negative_map, cube->m_z_positive_map, cube->m_z_negative_map};
+        size_t fb = (size_t)cube->length * cube->length * 4;
+        for (int f = 0; f < 6; f++) {
+            if (!faces[f]) { set_error("cube map face %d is null", f); return PT_E_ARG; }
+            st.cube.insert(st.cube.end(), faces[f], faces[f] + fb);
+        }
+        st.cube_len = cube->length;
+    }
+    return PT_OK;
+}
+
+DevConfig to_dev(const pt_configuration& c) {
+    DevConfig d;
+    d.max_depth = c.max_tracer_depth;
+    d.bias = c.vector_bias_length;
+    d.energy_threshold = c.energy_exist_threshold;
+    d.sss_threshold = c.sss_threshold;
+    d.use_sky_box = c.use_sky_box;
+    d.use_sky = c.use_sky;
+    d.use_bilinear = c.use_bilinear;
+    d.gamma_correction = c.gamma_correction;
+    d.use_anti_alias = c.use_anti_alias;
+    d.air_n = c.air_refraction_index;
+    d.air_absorption[0] = c.air_absorption_coef.x; d.air_absorption[1] = c.air_absorption_coef.y;
+    d.air_absorption[2] = c.air_absorption_coef.z;
+    d.air_reduced_scattering[0] = c.air_reduced_scattering_coef.x;
+    d.air_reduced_scattering[1] = c.air_reduced_scattering_coef.y;
+    d.air_reduced_scattering[2] = c.air_reduced_scattering_coef.z;
+    return d;
+}
+
+// generate_ray_kernel :337-345 — camera-only terms, computed once with the device's arithmetic.
+DevCamera to_dev(const pt_render_camera& c) {
+    DevCamera d;
+    v3 eye = mk3(c.eye.x, c.eye.y, c.eye.z), view = mk3(c.view.x, c.view.y, c.view.z), up = mk3(c.up.x, c.up.y, c.up.z);
+    float distance = length(view);
+    v3 horizontal = normalize(cross(view, up));
+    v3 vertical = normalize(cross(horizontal, view));
+    v3 xa = horizontal * (distance * tan_pt(c.fov.x * 0.5f * (kPI / 180.0f)));
+    v3 ya = vertical * (distance * tan_pt(-c.fov.y * 0.5f * (kPI / 180.0f)));
+    float* dst[6] = {d.eye, d.view, d.horizontal, d.vertical, d.x_axis, d.y_axis};
+    v3 src[6] = {eye, view, horizontal, vertical, xa, ya};
+    for (int i = 0; i < 6; i++) { dst[i][0] = src[i].x; dst[i][1] = src[i].y; dst[i][2] = src[i].z; }
+    d.res_x = c.resolution.x;
+    d.res_y = c.resolution.y;
+    d.aperture = c.aperture_radius;
+    d.focal = c.focal_distance;
+    return d;
+}
+
+}  // namespace
+
+struct pt_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // scene
+    void* scene_mem = nullptr;
+    size_t scene_bytes = 0;
+    DevScene scene{};
+    int node_num = 0, tri_num = 0;
+    bool has_scene = false;
+    // frame
+    int width = 0, height = 0;
+    float* image = nullptr;        // float3
+    uint8_t* image256 = nullptr;   // uchar3
+    bool own_image = false;
+    size_t image_cap = 0, image256_cap = 0;
+    DevTiling tiling{0, 0, 1, 1, 0, 0};
+    // counters
+    unsigned int* fetch = nullptr;
+    unsigned long long* stats = nullptr;
+    bool instrumented = false;
+    int grid[2][2] = {{0, 0}, {0, 0}};
+    std::vector<hipEvent_t> ev_start, ev_stop;
+    size_t ev_used = 0;
+    // thread_shrink scratch
+    int* shrink_buf = nullptr;
+    int* shrink_tiles = nullptr;
+    int* shrink_total = nullptr;
+    size_t shrink_cap = 0;
+    // reference-ABI scene cache key
+    const void* key[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    int key_counts[2] = {-1, -1};
+    // reference-ABI host mirrors
+    const void* mirror_host = nullptr;
+};
+
+namespace {
+
+int ensure_device(pt_context* ctx) {
+    PT_HIP(hipSetDevice(ctx->device));
+    return PT_OK;
+}
+
+void free_scene(pt_context* ctx) {
+    if (ctx->scene_mem) (void)hipFree(ctx->scene_mem);
+    ctx->scene_mem = nullptr;
+    ctx->scene_bytes = 0;
+    ctx->has_scene = false;
+    std::memset(&ctx->scene, 0, sizeof(ctx->scene));
+}
+
+int upload_stage(pt_context* ctx, const SceneStage& st) {
+    struct Piece { const void* src; size_t bytes; size_t off; };
+    std::vector<Piece> pieces;
+    size_t total = 0;
+    auto add = [&](const void* p, size_t b) {
+        size_t off = (total + 255) & ~(size_t)255;
+        pieces.push_back({p, b, off});
+        total = off + b;
+        return pieces.size() - 1;
+    };
+    size_t i_nodes = add(st.nodes.data(), st.nodes.size() * sizeof(float4));
+    size_t i_leaf = add(st.leaf_tris.data(), st.leaf_tris.size() * sizeof(int));
+    size_t i_range = add(st.mesh_range.data(), st.mesh_range.size() * sizeof(int2));
+    size_t i_geom = add(st.tri_geom.data(), st.tri_geom.size() * sizeof(float4));
+    size_t i_shade = add(st.tri_shade.data(), st.tri_shade.size() * sizeof(float4));
+    size_t i_sph = add(st.spheres.data(), st.spheres.size() * sizeof(float4));
+    size_t i_mat = add(st.mats.data(), st.mats.size() * sizeof(DevMaterial));
+    size_t i_tex = add(st.tex_desc.data(), st.tex_desc.size() * sizeof(int4));
+    size_t i_pool = add(st.tex_pool.data(), st.tex_pool.size());
+    size_t i_cube = add(st.cube.data(), st.cube.size());
+    free_scene(ctx);
+    if (total == 0) total = 256;
+    PT_HIP(hipMalloc(&ctx->scene_mem, total));
+    ctx->scene_bytes = total;
+    uint8_t* base = (uint8_t*)ctx->scene_mem;
+    for (const Piece& p : pieces)
+        if (p.bytes) PT_HIP(hipMemcpyAsync(base + p.off, p.src, p.bytes, hipMemcpyHostToDevice, ctx->stream));
+    PT_HIP(hipStreamSynchronize(ctx->stream));
+    DevScene& s = ctx->scene;
+    s.nodes = (const float4*)(base + pieces[i_nodes].off);
+    s.leaf_tris = (const int*)(base + pieces[i_leaf].off);
+    s.mesh_range = (const int2*)(base + pieces[i_range].off);
+    s.tri_geom = (const float4*)(base + pieces[i_geom].off);
+    s.tri_shade = (const float4*)(base + pieces[i_shade].off);
+    s.spheres = (const float4*)(base + pieces[i_sph].off);
+    s.materials = (const DevMaterial*)(base + pieces[i_mat].off);
+    s.tex_desc = (const int4*)(base + pieces[i_tex].off);
+    s.tex_pool = (const uint8_t*)(base + pieces[i_pool].off);
+    s.cube = (const uint8_t*)(base + pieces[i_cube].off);
+    s.mesh_num = (int)st.mesh_range.size();
+    s.sphere_num = (int)(st.spheres.size() / 2);
+    s.leaf_size = st.leaf_size;
+    s.cube_len = st.cube_len;
+    ctx->node_num = (int)(st.nodes.size() / 2);
+    ctx->tri_num = (int)(st.tri_geom.size() / 3);
+    ctx->has_scene = true;
+    return PT_OK;
+}
+
+int ensure_image(pt_context* ctx, int width, int height, void* external) {
+    size_t px = (size_t)width * height;
+    if (external) {
+        if (ctx->own_image && ctx->image) (void)hipFree(ctx->image);
+        ctx->image = (float*)external;
+        ctx->own_image = false;
+        ctx->image_cap = px;
+    } else if (!ctx->own_image || ctx->image_cap < px) {
+        if (ctx->own_image && ctx->image) (void)hipFree(ctx->image);
+        ctx->image = nullptr;
+        PT_HIP(hipMalloc(&ctx->image, px * 12));
+        PT_HIP(hipMemsetAsync(ctx->image, 0, px * 12, ctx->stream));
+        ctx->own_image = true;
+        ctx->image_cap = px;
+    }
+    if (ctx->image256_cap < px) {
+        if (ctx->image256) (void)hipFree(ctx->image256);
+        ctx->image256 = nullptr;
+        PT_HIP(hipMalloc(&ctx->image256, px * 3));
+        ctx->image256_cap = px;
+    }
+    ctx->width = width;
+    ctx->height = height;
+    return PT_OK;
+}
+
+void update_tiling(pt_context* ctx) {
+    DevTiling& t = ctx->tiling;
+    t.width = ctx->width;
+    t.height = ctx->height;
+    if (t.band_count <= 1) {
+        t.band_count = 1;
+        t.band_index = 0;
+        t.unit_count = ctx->width * ctx->height;
+        return;
+    }
+    // rows y with (y / band_rows) % band_count == band_index, enumerated band by band
+    int rows = 0;
+    for (int y = 0; y < ctx->height; y++)
+        if ((y / t.band_rows) % t.band_count == t.band_index) rows++;
+    t.unit_count = rows * ctx->width;
+}
+
+int pass_grid(pt_context* ctx) {
+    bool leaf1 = ctx->scene.leaf_size == 1;
+    int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0];
+    if (g == 0) g = pass_grid_size(leaf1, ctx->instrumented);
+    return g;
+}
+
+int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config, int first_pass,
+                  int pass_count, int write_u8) {
+    if (!ctx->has_scene) { set_error("no scene uploaded"); return PT_E_STATE; }
+    if (!ctx->image) { set_error("no frame set up"); return PT_E_STATE; }
+    if (!cam || !config) { set_error("null camera/config"); return PT_E_ARG; }
+    if ((int)cam->resolution.x != ctx->width) { set_error("camera width != frame width"); return PT_E_ARG; }
+    DevConfig dc = to_dev(*config);
+    DevCamera dcam = to_dev(*cam);
+    update_tiling(ctx);
+    DevOutput out;
+    out.image = ctx->image;
+    out.image256 = ctx->image256;
+    out.fetch = ctx->fetch;
+    out.stats = ctx->stats;
+    const int grid = pass_grid(ctx);
+    for (int i = 0; i < pass_count; i++) {
+        int pass = first_pass + i;
+        int w8 = write_u8 == 1 || (write_u8 == 2 && i == pass_count - 1);
+        PT_HIP(hipMemsetAsync(ctx->fetch, 0, sizeof(unsigned int), ctx->stream));
+        if (ctx->ev_used == ctx->ev_start.size()) {
+            hipEvent_t a, b;
+            PT_HIP(hipEventCreate(&a));
+            PT_HIP(hipEventCreate(&b));
+            ctx->ev_start.push_back(a);
+            ctx->ev_stop.push_back(b);
+        }
+        PT_HIP(hipEventRecord(ctx->ev_start[ctx->ev_used], ctx->stream));
+        PT_HIP(launch_pass(ctx->scene, dc, dcam, ctx->tiling, out, pass, w8, grid, ctx->instrumented, ctx->stream));
+        PT_HIP(hipEventRecord(ctx->ev_stop[ctx->ev_used], ctx->stream));
+        ctx->ev_used++;
+    }
+    return PT_OK;
+}
+
+std::mutex g_default_mutex;
+pt_context* g_default = nullptr;
+
+pt_context* default_context() {
+    std::lock_guard<std::mutex> lock(g_default_mutex);
+    if (!g_default) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+        if (pt_context_create(dev, &g_default) != PT_OK) g_default = nullptr;
+    }
+    return g_default;
+}
+
+void report(const char* where) {
+    std::fprintf(stderr, "%s (%s)\n", g_last_error.c_str(), where);
+}
+
+bool is_device_memory(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice;
+}
+
+}  // namespace
+
+// =============================================================================================
+// native C-ABI
+extern "C" const char* pt_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int pt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" int pt_context_create(int device, pt_context** out) {
+    if (!out) { set_error("null out"); return PT_E_ARG; }
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) { set_error("[Hip]Error no HIP device available"); return PT_E_HIP; }
+    if (device < 0 || device >= n) { set_error("device %d out of range", device); return PT_E_ARG; }
+    pt_context* ctx = new pt_context();
+    ctx->device = device;
+    int rc = ensure_device(ctx);
+    if (rc == PT_OK && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { set_error("stream"); rc = PT_E_HIP; }
+    if (rc == PT_OK && hipMalloc(&ctx->fetch, 256) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
+    if (rc == PT_OK && hipMalloc(&ctx->stats, 256) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
+    if (rc == PT_OK && hipMemset(ctx->stats, 0, 256) != hipSuccess) { set_error("memset"); rc = PT_E_HIP; }
+    if (rc != PT_OK) { pt_context_destroy(ctx); return rc; }
+    *out = ctx;
+    return PT_OK;
+}
+
+extern "C" void pt_context_destroy(pt_context* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    free_scene(ctx);
+    if (ctx->own_image && ctx->image) (void)hipFree(ctx->image);
+    if (ctx->image256) (void)hipFree(ctx->image256);
+    if (ctx->fetch) (void)hipFree(ctx->fetch);
+    if (ctx->stats) (void)hipFree(ctx->stats);
+    if (ctx->shrink_buf) (void)hipFree(ctx->shrink_buf);
+    if (ctx->shrink_tiles) (void)hipFree(ctx->shrink_tiles);
+    if (ctx->shrink_total) (void)hipFree(ctx->shrink_total);
+    for (auto e : ctx->ev_start) (void)hipEventDestroy(e);
+    for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+extern "C" int pt_scene_upload(pt_context* ctx, int mesh_num, pt_bvh_node_device** bvh_nodes, pt_triangle* triangles,
+                               int triangle_num, int sphere_num, pt_sphere* spheres, pt_cube_map* sky_cube_map,
+                               pt_texture_wrapper* mesh_textures, int texture_num, const pt_configuration* config) {
+    if (!ctx || !config) { set_error("null context/config"); return PT_E_ARG; }
+    int rc = ensure_device(ctx);
+    if (rc != PT_OK) return rc;
+    SceneStage st;
+    rc = translate_scene(st, mesh_num, bvh_nodes, triangles, triangle_num, sphere_num, spheres, sky_cube_map,
+                         mesh_textures, texture_num, config);
+    if (rc != PT_OK) return rc;
+    return upload_stage(ctx, st);
+}
+
+extern "C" int pt_scene_info(pt_context* ctx, long long* bytes, int* node_num, int* triangle_num) {
+    if (!ctx) return PT_E_ARG;
+    if (bytes) *bytes = (long long)ctx->scene_bytes;
+    if (node_num) *node_num = ctx->node_num;
+    if (triangle_num) *triangle_num = ctx->tri_num;
+    return PT_OK;
+}
+
+extern "C" int pt_frame_setup(pt_context* ctx, int width, int height, void* image_device) {
+    if (!ctx || width <= 0 || height <= 0) { set_error("bad frame size"); return PT_E_ARG; }
+    int rc = ensure_device(ctx);
+    if (rc != PT_OK) return rc;
+    return ensure_image(ctx, width, height, image_device);
+}
+
+extern "C" int pt_set_tiling(pt_context* ctx, int band_rows, int band_count, int band_index) {
+    if (!ctx || band_rows <= 0 || band_count <= 0 || band_index < 0 || band_index >= band_count) {
+        set_error("bad tiling");
+        return PT_E_ARG;
+    }
+    ctx->tiling.band_rows = band_rows;
+    ctx->tiling.band_count = band_count;
+    ctx->tiling.band_index = band_index;
+    return PT_OK;
+}
+
+extern "C" int pt_render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config,
+                                int first_pass, int pass_count, int write_u8) {
+    if (!ctx || first_pass < 1 || pass_count < 0) { set_error("bad pass range"); return PT_E_ARG; }
+    int rc = ensure_device(ctx);
+    if (rc != PT_OK) return rc;
+    return render_passes(ctx, cam, config, first_pass, pass_count, write_u8);
+}
+
+extern "C" int pt_finalize_u8(pt_context* ctx, const pt_configuration* config, int pass) {
+    if (!ctx || !config || pass < 1) return PT_E_ARG;
+    int rc = ensure_device(ctx);
+    if (rc != PT_OK) return rc;
+    PT_HIP(launch_u8(to_dev(*config), ctx->image, ctx->image256, ctx->width * ctx->height, pass, ctx->stream));
+    return PT_OK;
+}
+
+extern "C" int pt_synchronize(pt_context* ctx) {
+    if (!ctx) return PT_E_ARG;
+    PT_HIP(hipSetDevice(ctx->device));
+    PT_HIP(hipStreamSynchronize(ctx->stream));
+    return PT_OK;
+}
+
+extern "C" int pt_image_download(pt_context* ctx, pt_float3* image, pt_uchar3* image256) {
+    if (!ctx || !ctx->image) return PT_E_STATE;
+    PT_HIP(hipSetDevice(ctx->device));
+    size_t px = (size_t)ctx->width * ctx->height;
+    if (image) PT_HIP(hipMemcpyAsync(image, ctx->image, px * 12, hipMemcpyDeviceToHost, ctx->stream));
+    if (image256) PT_HIP(hipMemcpyAsync(image256, ctx->image256, px * 3, hipMemcpyDeviceToHost, ctx->stream));
+    PT_HIP(hipStreamSynchronize(ctx->stream));
+    return PT_OK;
+}
+
+extern "C" void* pt_image_device_ptr(pt_context* ctx) { return ctx ? ctx->image : nullptr; }
+extern "C" void* pt_image256_device_ptr(pt_context* ctx) { return ctx ? ctx->image256 : nullptr; }
+
+extern "C" int pt_stats_reset(pt_context* ctx) {
+    if (!ctx) return PT_E_ARG;
+    PT_HIP(hipSetDevice(ctx->device));
+    PT_HIP(hipStreamSynchronize(ctx->stream));
+    PT_HIP(hipMemsetAsync(ctx->stats, 0, 256, ctx->stream));
+    PT_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->ev_used = 0;
+    return PT_OK;
+}
+
+extern "C" int pt_stats_all(pt_context* ctx, unsigned long long* out, int n) {
+    if (!ctx || !out || n < 0 || n > 32) return PT_E_ARG;
+    PT_HIP(hipSetDevice(ctx->device));
+    PT_HIP(hipMemcpyAsync(out, ctx->stats, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+    PT_HIP(hipStreamSynchronize(ctx->stream));
+    return PT_OK;
+}
+
+extern "C" int pt_stats(pt_context* ctx, unsigned long long* segments, unsigned long long* nodes, unsigned long long* tris) {
+    if (!ctx) return PT_E_ARG;
+    unsigned long long h[4] = {0, 0, 0, 0};
+    PT_HIP(hipSetDevice(ctx->device));
+    PT_HIP(hipMemcpyAsync(h, ctx->stats, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+    PT_HIP(hipStreamSynchronize(ctx->stream));
+    if (segments) *segments = h[0];
+    if (nodes) *nodes = h[1];
+    if (tris) *tris = h[2];
+    return PT_OK;
+}
+
+extern "C" int pt_set_instrumented(pt_context* ctx, int on) {
+    if (!ctx) return PT_E_ARG;
+    ctx->instrumented = on != 0;
+    return PT_OK;
+}
+
+extern "C" int pt_kernel_time(pt_context* ctx, double* total_ms, int* launches) {
+    if (!ctx) return PT_E_ARG;
+    PT_HIP(hipSetDevice(ctx->device));
+    double t = 0.0;
+    for (size_t i = 0; i < ctx->ev_used; i++) {
+        PT_HIP(hipEventSynchronize(ctx->ev_stop[i]));
+        float ms = 0.0f;
+        PT_HIP(hipEventElapsedTime(&ms, ctx->ev_start[i], ctx->ev_stop[i]));
+        t += ms;
+    }
+    if (total_ms) *total_ms = t;
+    if (launches) *launches = (int)ctx->ev_used;
+    return PT_OK;
+}
+
+extern "C" int pt_math_eval_device(pt_context* ctx, int which, const float* x, int n, float* out0, float* out1) {
+    if (!ctx || !x || n < 0 || !out0 || !out1) { set_error("bad math_eval args"); return PT_E_ARG; }
+    PT_HIP(hipSetDevice(ctx->device));
+    float* d = nullptr;
+    size_t b = (size_t)n * sizeof(float);
+    PT_HIP(hipMalloc(&d, 3 * b + 16));
+    hipError_t e = hipMemcpy(d, x, b, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_math_eval(which, d, n, d + n, d + 2 * (size_t)n, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipMemcpy(out0, d + n, b, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out1, d + 2 * (size_t)n, b, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    PT_HIP(e);
+    return PT_OK;
+}
+
+// =============================================================================================
+// reference C-ABI (include/path_tracer_kernel.h)
+extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_device, pt_triangle* triangles_device,
+                                   int sphere_num, pt_sphere* spheres_device, int pixel_count, pt_float3* image_pixels,
+                                   pt_uchar3* image_pixels_256, int pass_counter, pt_render_camera* render_camera_device,
+                                   pt_cube_map* sky_cube_map_device, pt_float3* not_absorbed_colors_device,
+                                   pt_float3* accumulated_colors_device, pt_ray* rays_device,
+                                   int* energy_exist_pixels_device, pt_scattering* scatterings_device,
+                                   pt_texture_wrapper* mesh_textures_device, pt_configuration* config_device) {
+    (void)not_absorbed_colors_device; (void)accumulated_colors_device; (void)rays_device;
+    (void)energy_exist_pixels_device; (void)scatterings_device;
+    pt_context* ctx = default_context();
+    if (!ctx) { report("path_tracer_kernel: context"); return; }
+    if (!config_device || !render_camera_device || pixel_count <= 0) {
+        set_error("[Hip]Error invalid argument to path_tracer_kernel");
+        report("path_tracer_kernel");
+        return;
+    }
+    const pt_configuration config = *config_device;  // host read, as :706
+    const pt_render_camera cam = *render_camera_device;
+    const void* key[6] = {bvh_nodes_device, triangles_device, spheres_device, sky_cube_map_device, mesh_textures_device,
+                          nullptr};
+    bool same = ctx->has_scene && ctx->key_counts[0] == mesh_num && ctx->key_counts[1] == sphere_num;
+    for (int i = 0; i < 5 && same; i++) same = ctx->key[i] == key[i];
+    if (!same || pass_counter == 1) {
+        int rc = pt_scene_upload(ctx, mesh_num, bvh_nodes_device, triangles_device, -1, sphere_num, spheres_device,
+                                 sky_cube_map_device, mesh_textures_device, -1, &config);
+        if (rc != PT_OK) { report("path_tracer_kernel: scene"); return; }
+        for (int i = 0; i < 6; i++) ctx->key[i] = key[i];
+        ctx->key_counts[0] = mesh_num;
+        ctx->key_counts[1] = sphere_num;
+    }
+    const int width = (int)cam.resolution.x;
+    if (width <= 0 || pixel_count % width != 0) {
+        set_error("[Hip]Error pixel_count %d is not a multiple of the camera width %d", pixel_count, width);
+        report("path_tracer_kernel");
+        return;
+    }
+    const int height = pixel_count / width;
+    const bool direct = is_device_memory(image_pixels) && is_device_memory(image_pixels_256);
+    int rc = ensure_image(ctx, width, height, direct ? (void*)image_pixels : nullptr);
+    if (rc != PT_OK) { report("path_tracer_kernel: image"); return; }
+    uint8_t* own256 = ctx->image256;
+    if (direct) ctx->image256 = (uint8_t*)image_pixels_256;
+    ctx->tiling.band_count = 1;
+    rc = render_passes(ctx, &cam, &config, pass_counter, 1, 1);
+    if (rc == PT_OK) {
+        if (!direct) rc = pt_image_download(ctx, image_pixels, image_pixels_256);
+        else if (hipStreamSynchronize(ctx->stream) != hipSuccess) { set_error("[Hip]Error synchronize"); rc = PT_E_HIP; }
+    }
+    if (direct) { ctx->image256 = own256; ctx->image = nullptr; ctx->image_cap = 0; ctx->own_image = false; }
+    if (rc != PT_OK) report("path_tracer_kernel");
+}
+
+extern "C" void path_tracer_kernel_memory_allocate(pt_float3** not_absorbed, pt_float3** accumulated, pt_ray** rays,
+                                                   int** energy, pt_scattering** scatterings, int pixel_count) {
+    size_t n = pixel_count > 0 ? (size_t)pixel_count : 1;
+    struct A { void** p; size_t b; } a[5] = {{(void**)not_absorbed, n * sizeof(pt_float3)},
+                                             {(void**)accumulated, n * sizeof(pt_float3)},
+                                             {(void**)rays, n * sizeof(pt_ray)},
+                                             {(void**)energy, n * sizeof(int)},
+                                             {(void**)scatterings, n * sizeof(pt_scattering)}};
+    for (auto& x : a) {
+        if (!x.p) continue;
+        *x.p = nullptr;
+        hipError_t e = hipMalloc(x.p, x.b);
+        if (e != hipSuccess) std::fprintf(stderr, "[Hip]Error %s in path_tracer_kernel_memory_allocate\n", hipGetErrorString(e));
+    }
+}
+
+extern "C" void path_tracer_kernel_memory_free(pt_float3* not_absorbed, pt_float3* accumulated, pt_ray* rays, int* energy,
+                                               pt_scattering* scatterings) {
+    void* p[5] = {not_absorbed, accumulated, rays, energy, scatterings};
+    for (void* x : p) {
+        if (!x) continue;
+        hipError_t e = hipFree(x);
+        if (e != hipSuccess) std::fprintf(stderr, "[Hip]Error %s in path_tracer_kernel_memory_free\n", hipGetErrorString(e));
+    }
+}
+
+extern "C" int thread_shrink(int* energy_exist_pixels_device, int energy_exist_pixels_count) {
+    pt_context* ctx = default_context();
+    if (!ctx) { report("thread_shrink: context"); return energy_exist_pixels_count; }
+    if (energy_exist_pixels_count <= 0 || !energy_exist_pixels_device) return 0;
+    if (hipSetDevice(ctx->device) != hipSuccess) { set_error("[Hip]Error set device"); report("thread_shrink"); return energy_exist_pixels_count; }
+    size_t n = (size_t)energy_exist_pixels_count;
+    if (ctx->shrink_cap < n) {
+        if (ctx->shrink_buf) (void)hipFree(ctx->shrink_buf);
+        if (ctx->shrink_tiles) (void)hipFree(ctx->shrink_tiles);
+        ctx->shrink_buf = nullptr; ctx->shrink_tiles = nullptr;
+        if (hipMalloc(&ctx->shrink_buf, n * sizeof(int)) != hipSuccess ||
+            hipMalloc(&ctx->shrink_tiles, ((n + 255) / 256) * sizeof(int)) != hipSuccess) {
+            set_error("[Hip]Error out of memory in thread_shrink");
+            report("thread_shrink");
+            ctx->shrink_cap = 0;
+            return energy_exist_pixels_count;
+        }
+        ctx->shrink_cap = n;
+    }
+    if (!ctx->shrink_total && hipMalloc(&ctx->shrink_total, sizeof(int)) != hipSuccess) {
+        set_error("[Hip]Error out of memory in thread_shrink");
+        report("thread_shrink");
+        return energy_exist_pixels_count;
+    }
+    int total = 0;
+    hipError_t e = shrink(energy_exist_pixels_device, energy_exist_pixels_count, ctx->shrink_buf, ctx->shrink_tiles,
+                          ctx->shrink_total, &total, ctx->stream);
+    if (e != hipSuccess) {
+        set_error("[Hip]Error %s in thread_shrink", hipGetErrorString(e));
+        report("thread_shrink");
+        return energy_exist_pixels_count;
+    }
+    return total;
+}

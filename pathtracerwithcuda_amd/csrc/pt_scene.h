@@ -1,0 +1,116 @@
+// pt_scene.h — the device-resident scene layout and kernel parameter blocks.
+//
+// The reference keeps AoS structs in managed memory with embedded pointers (triangle.mat,
+// bvh_node_device.triangle_indices, the per-mesh bvh_node_device** table, cube_map face
+// pointers, texture_wrapper.pixels). Here everything is relocated into a
+// handful of hipMalloc'd arrays addressed by 32-bit indices:
+//
+//   nodes      float4[2*N]  node i = {lb.xyz, next_node_index (int bits)},
+//                                    {rt.xyz, leaf ? leaf_slot : -1 (int bits)}   32 B/node
+//              all meshes concatenated; next indices are absolute; mesh m spans
+//              [mesh_range[m].x, mesh_range[m].y)  (reference: bvh_nodes[m][0].next_node_index)
+//   leaf_tris  int[L*leaf_size]  triangle ids per leaf, -1 padded (bvh.cpp:296-300)
+//              when leaf_size == 1 the slot field holds the triangle id directly
+//   tri_geom   float4[3*T]  {v0.xyz, -}, {v1-v0}, {v2-v0}                       48 B/tri
+//   tri_shade  float4[4*T]  {n0.xyz, n1.x}, {n1.yz, n2.xy}, {n2.z, uv0.xy, uv1.x},
+//                           {uv1.y, uv2.xy, material id (int bits)}             64 B/tri
+//   spheres    float4[2*S]  {center.xyz, radius}, {material id, -, -, -}
+//   materials  DevMaterial[M] (96 B), sphere materials appended after mesh materials
+//   textures   int4[K] {width, height, byte offset, -} + one RGBA8 byte pool
+//   cube       RGBA8, 6 faces back to back (x+, x-, y+, y-, z+, z-), length^2 texels each
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#else
+struct alignas(16) float4 { float x, y, z, w; };
+struct alignas(8) int2 { int x, y; };
+struct alignas(16) int4 { int x, y, z, w; };
+#endif
+
+namespace pt {
+
+struct alignas(16) DevMaterial {
+    float diffuse[3];
+    float roughness;
+    float emission[3];
+    float refraction_index;
+    float specular[3];
+    float extinction_coefficient;
+    float absorption[3];
+    float reduced_scattering[3];
+    int is_transparent;
+    int diffuse_texture_id;
+    int specular_texture_id;
+    int pad[3];
+};
+static_assert(sizeof(DevMaterial) == 96, "DevMaterial layout");
+
+struct DevScene {
+    const float4* nodes;
+    const int* leaf_tris;
+    const int2* mesh_range;
+    const float4* tri_geom;
+    const float4* tri_shade;
+    const float4* spheres;
+    const DevMaterial* materials;
+    const int4* tex_desc;
+    const uint8_t* tex_pool;
+    const uint8_t* cube;
+    int mesh_num;
+    int sphere_num;
+    int leaf_size;
+    int cube_len;
+};
+
+// The subset of Core/configuration.h:9-34 that the kernel reads.
+struct DevConfig {
+    int max_depth;
+    float bias;
+    float energy_threshold;
+    float sss_threshold;
+    int use_sky_box;
+    int use_sky;
+    int use_bilinear;
+    int gamma_correction;
+    int use_anti_alias;
+    float air_n;
+    float air_absorption[3];
+    float air_reduced_scattering[3];
+};
+
+// Core/camera.h:14-23 plus the per-frame canvas terms generate_ray_kernel derives
+// (path_tracer_kernel.cu:337-345): they depend only on the camera, so they are computed once.
+struct DevCamera {
+    float eye[3];
+    float view[3];
+    float horizontal[3];
+    float vertical[3];
+    float x_axis[3];
+    float y_axis[3];
+    float res_x, res_y;
+    float aperture;
+    float focal;
+};
+
+// Which pixels this launch owns: the frame is cut into bands of band_rows rows dealt
+// round-robin over band_count owners; owner band_index takes its share. Single GPU: 1 / 0.
+struct DevTiling {
+    int width;
+    int height;
+    int band_rows;
+    int band_count;
+    int band_index;
+    int unit_count;  // pixels owned
+};
+
+struct DevOutput {
+    float* image;            // float3 running sum, reference layout (12 B stride)
+    uint8_t* image256;       // uchar3 (3 B stride), may be null
+    unsigned int* fetch;     // work counter (zeroed before launch)
+    unsigned long long* stats;  // [0] ray segments, [1..] optional instrumentation
+};
+
+}  // namespace pt

@@ -1,0 +1,135 @@
+"""Host-side driver of the render call — the headless counterpart of Core/path_tracer.cpp:18-99
+(init / render / clear) on top of libpt_hip.so's native C-ABI (include/pt_native.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from ._abi import Configuration, RenderCamera, ViewCamera, check, lib
+from .scene import Scene
+
+
+def configuration(**overrides) -> Configuration:
+    """res/configuration/config.json defaults (pt_configuration_default) with field overrides."""
+    cfg = Configuration()
+    lib().pt_configuration_default(C.byref(cfg))
+    for k, v in overrides.items():
+        if not hasattr(cfg, k):
+            raise AttributeError(f"configuration has no field {k!r}")
+        if k in ("air_absorption_coef", "air_reduced_scattering_coef"):
+            v = _abi.Float3(*map(float, v))
+        setattr(cfg, k, v)
+    return cfg
+
+
+def camera(width: int, height: int, fov: float = 45.0, yaw: float = 0.0, pitch: float = 0.3, radius: float = 14.0,
+           center=(0.0, 0.0, 0.0), aperture: float = 0.0, focal: float | None = None) -> RenderCamera:
+    """view_camera defaults (Core/camera.cpp:3-14) -> render_camera (:80-98); FOV as window.cpp:356-360."""
+    vc = ViewCamera()
+    L = lib()
+    L.pt_view_camera_default(C.byref(vc))
+    vc.center = _abi.Float3(*map(float, center))
+    vc.yaw, vc.pitch, vc.radius = float(yaw), float(pitch), float(radius)
+    vc.aperture_radius = float(aperture)
+    vc.focal_distance = float(radius if focal is None else focal)
+    L.pt_view_camera_set_resolution(C.byref(vc), float(width), float(height))
+    L.pt_view_camera_set_fov(C.byref(vc), float(fov))
+    rc = RenderCamera()
+    L.pt_view_camera_get_render_camera(C.byref(vc), C.byref(rc))
+    return rc
+
+
+class Renderer:
+    """One device context: resident scene, resident accumulation image, one HIP stream."""
+
+    def __init__(self, device: int = 0):
+        self._lib = lib()
+        ctx = C.c_void_p()
+        check(self._lib.pt_context_create(int(device), C.byref(ctx)), "pt_context_create")
+        self._ctx = ctx
+        self.width = self.height = 0
+
+    def close(self):
+        if self._ctx:
+            self._lib.pt_context_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, scene: Scene, config: Configuration) -> None:
+        v = scene.view
+        check(self._lib.pt_scene_upload(self._ctx, v.mesh_num, v.bvh_nodes, v.triangles, v.triangle_num,
+                                        v.sphere_num, v.spheres, v.sky_cube_map, v.mesh_textures, v.texture_num,
+                                        C.byref(config)), "pt_scene_upload")
+
+    def scene_info(self) -> dict:
+        b, n, t = C.c_longlong(), C.c_int(), C.c_int()
+        check(self._lib.pt_scene_info(self._ctx, C.byref(b), C.byref(n), C.byref(t)), "pt_scene_info")
+        return {"device_bytes": b.value, "nodes": n.value, "triangles": t.value}
+
+    def setup_frame(self, width: int, height: int, image_device_ptr: int | None = None) -> None:
+        check(self._lib.pt_frame_setup(self._ctx, width, height, C.c_void_p(image_device_ptr or 0)), "pt_frame_setup")
+        self.width, self.height = width, height
+
+    def set_tiling(self, band_rows: int, band_count: int, band_index: int) -> None:
+        check(self._lib.pt_set_tiling(self._ctx, band_rows, band_count, band_index), "pt_set_tiling")
+
+    def render(self, cam: RenderCamera, config: Configuration, first_pass: int = 1, pass_count: int = 1,
+               write_u8: int = 2) -> None:
+        check(self._lib.pt_render_passes(self._ctx, C.byref(cam), C.byref(config), first_pass, pass_count, write_u8),
+              "pt_render_passes")
+
+    def finalize_u8(self, config: Configuration, passes: int) -> None:
+        check(self._lib.pt_finalize_u8(self._ctx, C.byref(config), passes), "pt_finalize_u8")
+
+    def synchronize(self) -> None:
+        check(self._lib.pt_synchronize(self._ctx), "pt_synchronize")
+
+    def download(self) -> tuple[np.ndarray, np.ndarray]:
+        img = np.empty((self.height, self.width, 3), np.float32)
+        img8 = np.empty((self.height, self.width, 3), np.uint8)
+        check(self._lib.pt_image_download(self._ctx, img.ctypes.data, img8.ctypes.data), "pt_image_download")
+        return img, img8
+
+    def image_device_ptr(self) -> int:
+        return self._lib.pt_image_device_ptr(self._ctx) or 0
+
+    def stats_reset(self) -> None:
+        check(self._lib.pt_stats_reset(self._ctx), "pt_stats_reset")
+
+    def stats(self) -> dict:
+        s, n, t = C.c_ulonglong(), C.c_ulonglong(), C.c_ulonglong()
+        check(self._lib.pt_stats(self._ctx, C.byref(s), C.byref(n), C.byref(t)), "pt_stats")
+        return {"segments": s.value, "nodes": n.value, "tris": t.value}
+
+    def stats_all(self) -> dict:
+        a = (C.c_ulonglong * 7)()
+        check(self._lib.pt_stats_all(self._ctx, a, 7), "pt_stats_all")
+        keys = ("segments", "nodes", "tris", "hit_mesh", "hit_sphere", "miss", "scatter")
+        return dict(zip(keys, (int(x) for x in a)))
+
+    def set_instrumented(self, on: bool) -> None:
+        check(self._lib.pt_set_instrumented(self._ctx, 1 if on else 0), "pt_set_instrumented")
+
+    def math_eval_device(self, which: int, x: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        x = np.ascontiguousarray(x, np.float32)
+        o0, o1 = np.empty_like(x), np.empty_like(x)
+        check(self._lib.pt_math_eval_device(self._ctx, which, x.ctypes.data, len(x), o0.ctypes.data, o1.ctypes.data),
+              "pt_math_eval_device")
+        return o0, o1
+
+    def kernel_time(self) -> tuple[float, int]:
+        ms, n = C.c_double(), C.c_int()
+        check(self._lib.pt_kernel_time(self._ctx, C.byref(ms), C.byref(n)), "pt_kernel_time")
+        return ms.value, n.value
+
+
+def device_count() -> int:
+    return lib().pt_device_count()

@@ -1,0 +1,117 @@
+"""Pins the oracle (oracle/oracle.c) before it is trusted as the checker:
+- hash + thrust minstd / uniform_real_distribution streams against tests/golden/rng_thrust.json,
+  generated from rocThrust by tools/gen_rng_golden.cpp (the reference's RNG is Thrust's);
+- MSVC CRT rand() known-answer sequence (the reference CPU fallback's RNG);
+- the single-precision transcendentals against float64 numpy (documented error bounds);
+- oracle invariants (pixel independence, pass accumulation, thread-count determinism).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import pathtracerwithcuda_amd as pt
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_hash_matches_golden():
+    d = json.load(open(os.path.join(GOLD, "rng_thrust.json")))
+    for a, h in d["hash"]:
+        assert oracle.hash_(a) == h
+    assert oracle.hash_(1) == -1266253386
+
+
+def test_thrust_streams_match_rocthrust_golden():
+    d = json.load(open(os.path.join(GOLD, "rng_thrust.json")))
+    assert len(d["streams"]) > 100
+    for s in d["streams"]:
+        got = oracle.rng_stream("thrust", s["seed"], len(s["bits"]), s["a"], s["b"])
+        assert list(got.view(np.uint32)) == s["bits"], s["seed"]
+
+
+def test_msvc_rand_known_answer():
+    # MSVC CRT: srand(1); rand() -> 41, 18467, 6334, 26500, 19169, 15724, 11478, 29358, 26962, 24464
+    got = oracle.rng_stream("msvc", 1, 10)
+    assert list(got.astype(int)) == [41, 18467, 6334, 26500, 19169, 15724, 11478, 29358, 26962, 24464]
+
+
+@pytest.mark.parametrize("which,lo,hi,fn,tol", [
+    (1, -80.0, 80.0, np.exp, 4e-7),
+    (2, 1e-30, 1e30, np.log, 2e-7),
+    (3, -50.0, 50.0, np.arctan, 3e-7),
+    (4, -1.0, 1.0, np.arcsin, 4e-7),
+    (5, -1.0, 1.0, np.arccos, 4e-7),
+])
+def test_cephes_functions_accuracy(which, lo, hi, fn, tol):
+    rng = np.random.default_rng(which)
+    if which == 2:
+        x = (10.0 ** rng.uniform(-30, 30, 20000)).astype(np.float32)
+    else:
+        x = rng.uniform(lo, hi, 20000).astype(np.float32)
+    got, _ = oracle.math_eval(which, "cephes", x)
+    ref = fn(x.astype(np.float64))
+    err = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)
+    if which == 5:  # acos: absolute error near the 0 result
+        err = np.abs(got - ref)
+    assert np.nanmax(err) < tol
+
+
+def test_cephes_sincos_accuracy():
+    x = np.linspace(0.0, 2 * np.pi, 50001).astype(np.float32)
+    s, c = oracle.math_eval(0, "cephes", x)
+    xd = x.astype(np.float64)
+    assert np.max(np.abs(s - np.sin(xd))) < 3e-7
+    assert np.max(np.abs(c - np.cos(xd))) < 3e-7
+
+
+def test_cephes_special_values():
+    x = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-40, 100.0, -200.0], np.float32)
+    e, _ = oracle.math_eval(1, "cephes", x)
+    assert e[0] == 1.0 and e[2] == np.inf and e[3] == 0.0 and np.isnan(e[4]) and e[7] == 0.0
+    lg, _ = oracle.math_eval(2, "cephes", np.array([0.0, 1.0, -1.0, np.inf, 1e-40], np.float32))
+    assert lg[0] == -np.inf and lg[1] == 0.0 and np.isnan(lg[2]) and lg[3] == np.inf
+    assert abs(lg[4] - np.log(1e-40)) < 1e-4
+    p, _ = oracle.math_eval(6, "cephes", np.array([0.0, 1.0, 0.5], np.float32))
+    assert p[0] == 0.0 and p[1] == 1.0 and abs(p[2] - 0.5 ** 1.85) < 1e-6
+
+
+@pytest.fixture(scope="module")
+def small_scene():
+    return pt.cornell_scene(pt.torus_knot(40, 12), cube_length=32)
+
+
+def test_oracle_pixels_are_independent(small_scene):
+    cfg = pt.configuration(max_tracer_depth=5)
+    cam = pt.camera(48, 32, pitch=0.08, radius=12.5, center=(0, 1.2, 0))
+    full, full8, _ = oracle.render(small_scene.view, cam, cfg, 1, 2)
+    sel = np.array([0, 5, 100, 777, 1535, 1000], np.int32)
+    sub, sub8, _ = oracle.render(small_scene.view, cam, cfg, 1, 2, pixels=sel)
+    assert np.array_equal(sub, full[sel]) and np.array_equal(sub8, full8[sel])
+
+
+def test_oracle_pass_accumulation_and_threads(small_scene):
+    cfg = pt.configuration(max_tracer_depth=4)
+    cam = pt.camera(40, 24)
+    a, _, _ = oracle.render(small_scene.view, cam, cfg, 1, 3, threads=1)
+    b, _, _ = oracle.render(small_scene.view, cam, cfg, 1, 3, threads=8)
+    assert np.array_equal(a, b)
+    # pass_counter semantics: pass 1 overwrites, later passes add (path_tracer_kernel.cu:644-651)
+    p1, _, _ = oracle.render(small_scene.view, cam, cfg, 1, 1)
+    p2, _, _ = oracle.render(small_scene.view, cam, cfg, 2, 1)
+    p3, _, _ = oracle.render(small_scene.view, cam, cfg, 3, 1)
+    assert np.array_equal(a, (p1 + p2) + p3)
+
+
+def test_libm_mode_is_close_to_cephes(small_scene):
+    """Calibrates the float tolerance: swapping every transcendental for glibc's (1-ulp scale changes,
+    the same order as the reference's CUDA intrinsics) moves few pixels and the image mean barely."""
+    cfg = pt.configuration(max_tracer_depth=6)
+    cam = pt.camera(64, 48, pitch=0.08, radius=12.5, center=(0, 1.2, 0))
+    a, _, _ = oracle.render(small_scene.view, cam, cfg, 1, 4)
+    b, _, _ = oracle.render(small_scene.view, cam, cfg, 1, 4, math="libm")
+    d = np.abs(a - b)
+    assert (d.max(axis=1) <= 1e-3).mean() >= 0.97
+    assert abs(a.mean() - b.mean()) <= 0.02 * a.mean()
