@@ -4,7 +4,8 @@ reference's own C-ABI (include/path_tracer_kernel.h). See DESIGN.md.
 """
 from ._abi import LAYOUT, EXPORTED, PtError, lib  # noqa: F401
 from .renderer import Renderer, camera, configuration, device_count  # noqa: F401
-from .scene import PRESETS, Scene, Shape, cornell_scene, cube_shape, cornell_shapes, material, torus_knot  # noqa: F401
+from .scene import PRESETS, Scene, Shape, cornell_scene, cornell_spheres_scene, cube_shape, cornell_shapes  # noqa: F401
+from .scene import material, torus_knot  # noqa: F401
 from .scene import procedural_cube_map  # noqa: F401
 
 __all__ = ["Renderer", "Scene", "Shape", "camera", "configuration", "cornell_scene", "torus_knot", "material",
