@@ -44,6 +44,13 @@ def algorithmic_bytes(counts: dict, sphere_count: int, leaf_size: int, pixels: i
     return b + 115.0 * pixels * passes
 
 
+def extend_bytes(counts: dict, sphere_count: int) -> float:
+    """The BVH-walk share of the same model (what one wavefront extend launch must move): ray in 24 B,
+    16 B per sphere, 32 B per node, 4 + 36 B per triangle test, hit record out 16 B."""
+    seg = counts["segments"]
+    return (24.0 + 16.0 + 16.0 * sphere_count) * seg + 32.0 * counts["nodes"] + 40.0 * counts["tris"]
+
+
 def cpu_baseline(scene, cam, cfg, threads: int) -> dict:
     """The reference's CPU fallback semantics (Core/path_tracer_cpu.cpp: MSVC rand, libm), as
     restated by the oracle, on the same frame: one whole frame (all 8 passes), so ms/frame is measured,
@@ -81,6 +88,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--save-image", default="")
+    ap.add_argument("--schedule", choices=["persistent", "wavefront"], default=None,
+                    help="kernel schedule (default: the library's, PT_MODE)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -101,6 +110,8 @@ def main() -> int:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     r = pt.Renderer(local)
+    r.set_schedule(args.schedule)
+    schedule = r.schedule()
     scene = pt.cornell_scene(pt.torus_knot(*KNOT))
     cfg = pt.configuration(max_tracer_depth=DEPTH)
     cam = pt.camera(WIDTH, HEIGHT, **CAMERA)
@@ -145,7 +156,8 @@ def main() -> int:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     segments = r.stats()["segments"]
-    kernel_ms, launches = r.kernel_time()
+    # dominant kernel: the pass kernel (persistent schedule) or the BVH-walk extend kernel (wavefront)
+    kernel_ms, launches = r.kernel_time_kind(0 if schedule == "persistent" else 1)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
@@ -171,12 +183,18 @@ def main() -> int:
     value = segments / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1000.0
     avg_launch_s = kernel_ms / max(launches, 1) / 1000.0
-    # one launch = one pass over the frame (this rank's bands when tiled)
-    bytes_per_launch = algorithmic_bytes(counts, scene.view.sphere_num, cfg.bvh_leaf_node_triangle_num,
-                                         WIDTH * HEIGHT, SPP) / SPP / world
+    if schedule == "persistent":
+        # one launch = one pass over the frame (this rank's bands when tiled)
+        bytes_per_launch = algorithmic_bytes(counts, scene.view.sphere_num, cfg.bvh_leaf_node_triangle_num,
+                                             WIDTH * HEIGHT, SPP) / SPP / world
+        kernel_name = "pass_kernel<LEAF1=true,STATS=false,MINW=6>"
+    else:
+        # one launch = one depth of one pass; averaged over the SPP * DEPTH extend launches
+        bytes_per_launch = extend_bytes(counts, scene.view.sphere_num) / (SPP * DEPTH) / world
+        kernel_name = "extend_kernel<LEAF1=true,STATS=false>"
     achieved = bytes_per_launch / avg_launch_s / 1e9
     workload = f"cornell+knot{KNOT[0] * KNOT[1] * 2}_{WIDTH}x{HEIGHT}_spp{SPP}_d{DEPTH}"
-    traffic = load_traffic(workload)
+    traffic = load_traffic(workload + ("" if schedule == "persistent" else "/wavefront"))
     line = {
         "metric": "Mrays/sec + ms/frame @1920x1080, 8spp, 8-bounce; 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -196,6 +214,7 @@ def main() -> int:
                      f"{scene.triangle_count} triangles, {scene.view.sphere_num} spheres",
             "width": WIDTH, "height": HEIGHT, "spp": SPP, "max_depth": DEPTH,
             "parallelism": f"tiled{world}" if world > 1 else "single",
+            "schedule": schedule,
             "band_rows": BAND_ROWS if world > 1 else None,
             "ms_per_frame": round(ms_per_step, 3),
             "camera_samples_per_s_M": round(WIDTH * HEIGHT * SPP * args.steps / elapsed / 1e6, 3),
@@ -208,7 +227,7 @@ def main() -> int:
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "pass_kernel<LEAF1=true,STATS=false>",
+            "kernel": kernel_name,
             "avg_launch_ms": round(avg_launch_s * 1000, 4),
             "algorithmic_bytes_per_launch": round(bytes_per_launch),
             "counts_per_frame": counts,

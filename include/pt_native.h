@@ -68,8 +68,18 @@ int pt_stats(pt_context* ctx, unsigned long long* segments, unsigned long long* 
  * [5] misses, [6] subsurface scatter events ([1..6] instrumented kernel only). n <= 32. */
 int pt_stats_all(pt_context* ctx, unsigned long long* out, int n);
 int pt_set_instrumented(pt_context* ctx, int on);
+/* Kernel schedule of a pass (results are bit-identical under both):
+ *   PT_SCHEDULE_PERSISTENT  one persistent launch per pass, a path per lane (default)
+ *   PT_SCHEDULE_WAVEFRONT   per depth an extend (BVH walk) and a shade launch over ray queues
+ * -1 restores the default (environment PT_MODE=wave selects the wavefront). */
+#define PT_SCHEDULE_PERSISTENT 0
+#define PT_SCHEDULE_WAVEFRONT 1
+int pt_set_schedule(pt_context* ctx, int schedule);
+int pt_get_schedule(pt_context* ctx); /* the schedule render calls use, or < 0 on error */
 /* HIP-event time of the pass kernels since the last pt_stats_reset (on the stream they run on). */
 int pt_kernel_time(pt_context* ctx, double* total_ms, int* launches);
+/* The same per kernel kind: 0 single-kernel pass, 1 extend (BVH walk), 2 shade, 3 finalize; -1 all. */
+int pt_kernel_time_kind(pt_context* ctx, int kind, double* total_ms, int* launches);
 
 /* Diagnostic: evaluate the device transcendentals (which: 0 sincos, 1 exp, 2 log, 3 atan, 4 asin,
  * 5 acos, 6 pow(x,1.85), 7 tan, 8 sqrt & reciprocal) on n host floats; for the bitwise check

@@ -180,7 +180,10 @@ _PROTOS = {
     "pt_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
     "pt_stats_all": (C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]),
     "pt_set_instrumented":(C.c_int, [C.c_void_p, C.c_int]),
+    "pt_set_schedule":    (C.c_int, [C.c_void_p, C.c_int]),
+    "pt_get_schedule":    (C.c_int, [C.c_void_p]),
     "pt_kernel_time": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), c_int_p]),
+    "pt_kernel_time_kind": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double), c_int_p]),
     "pt_math_eval_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     # host (include/pt_host.h)
     "pt_bvh_build": (C.c_int, [C.POINTER(Triangle), C.c_int, C.c_int, C.c_int, C.c_int,

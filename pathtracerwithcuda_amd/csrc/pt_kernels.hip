@@ -13,16 +13,26 @@
 // (stable remove_if of dead pixels) done in-register, per wave, with no host synchronisation.
 // Results do not depend on the schedule: every random draw is seeded by (pass, pixel, depth)
 // (path_tracer_kernel.cu:324,415) and a pixel's passes are ordered by the launch sequence.
+#include <cstdlib>
+
 #include "pt_kernels.h"
 
 namespace pt {
 
-template <bool LEAF1, bool STATS>
-__global__ __launch_bounds__(PT_BLOCK) void pass_kernel(DevScene sc, DevConfig cfg, DevCamera cam, DevTiling til,
-                                                        DevOutput out, int pass, int write_u8) {
+// MINW = minimum waves per SIMD requested from the register allocator (0: compiler's choice);
+// the persistent loop is latency-bound, so occupancy is the first-order knob.
+template <bool LEAF1, bool STATS, int MINW, bool PREFETCH>
+__global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams* __restrict__ params, int pass,
+                                                              int write_u8, int chunk) {
     const int lane = threadIdx.x & 63;
+    // The launch parameters live in device memory and are re-read (scalar loads, K$ hits) inside
+    // every iteration instead of being pinned in SGPRs for the whole kernel: the empty asm makes
+    // the pointer opaque per iteration so loop-invariant code motion cannot hoist the fields.
+    const LaunchParams* P0 = params;
+    const DevConfig& cfg0 = P0->cfg;
+    const DevOutput& out0 = P0->out;
     const int32_t hseed = hash_pt(pass);
-    const float clamp_hi = (float)cfg.max_depth * 2.0f;
+    const float clamp_hi = (float)cfg0.max_depth * 2.0f;
     const unsigned long long lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
     PathState ps;
@@ -33,41 +43,40 @@ __global__ __launch_bounds__(PT_BLOCK) void pass_kernel(DevScene sc, DevConfig c
     unsigned long long segments = 0;
     Counters ctr = {0u, 0u, 0u, 0u, 0u, 0u};
     unsigned long long csum[6] = {0, 0, 0, 0, 0, 0};
+    // pixels in PT_SHARDS regions handed out in chunks (pt_work.h)
+    const unsigned int units = (unsigned int)P0->til.unit_count;
+    const EvenRegions regions{units, (units + PT_SHARDS - 1) / PT_SHARDS};
+    WorkCursor cursor = work_begin();
+    bool drained = false;
 
     while (true) {
+        const LaunchParams* P = params;
+        asm volatile("" : "+s"(P));
+        const DevScene& sc = P->sc;
+        const DevConfig& cfg = P->cfg;
+        const DevTiling& til = P->til;
+        const DevOutput& out = P->out;
         const bool want = need && !done;
         const unsigned long long need_mask = __ballot(want);
         if (need_mask) {
-            const int leader = __ffsll((long long)need_mask) - 1;
-            unsigned int base = 0;
-            if (lane == leader) base = atomicAdd(out.fetch, (unsigned int)__popcll(need_mask));
-            base = __shfl(base, leader);
+            const unsigned int u = work_take(out.fetch, regions.stride, regions, (unsigned int)chunk, need_mask, want,
+                                             lane_lt, cursor, drained);
             if (want) {
-                const unsigned int u = base + (unsigned int)__popcll(need_mask & lane_lt);
-                need = false;
-                if (u < (unsigned int)til.unit_count) {
-                    if (til.band_count == 1) {
-                        pixel = (int)u;
-                    } else {
-                        int row_local = (int)u / til.width;
-                        int x = (int)u - row_local * til.width;
-                        int band_local = row_local / til.band_rows;
-                        int row_in_band = row_local - band_local * til.band_rows;
-                        int y = (band_local * til.band_count + til.band_index) * til.band_rows + row_in_band;
-                        pixel = y * til.width + x;
-                    }
-                    generate_path(cam, cfg, pixel, hseed, &ps);
+                if (u != ~0u) {
+                    need = false;
+                    pixel = unit_to_pixel(til, u);
+                    generate_path(P->cam, cfg, pixel, hseed, &ps);
                     depth = 0;
-                } else {
+                } else if (drained) {
                     done = true;
                 }
             }
         }
         if (!__any(!done)) break;
-        if (!done) {
+        if (!done && !need) {  // a lane still waiting for a pixel (chunk ran short) has no path yet
             bool alive = false;
             if (depth < cfg.max_depth) {
-                alive = trace_step<LEAF1, STATS>(sc, cfg, pixel, depth, hseed, &ps, &ctr);
+                alive = trace_step<LEAF1, STATS, PREFETCH>(sc, cfg, pixel, depth, hseed, &ps, &ctr);
                 depth++;
                 segments++;
                 if (STATS) {
@@ -99,10 +108,10 @@ __global__ __launch_bounds__(PT_BLOCK) void pass_kernel(DevScene sc, DevConfig c
             for (int off = 32; off > 0; off >>= 1) csum[k] += __shfl_xor(csum[k], off);
     }
     if (lane == 0) {
-        atomicAdd(&out.stats[0], s);
+        atomicAdd(&out0.stats[0], s);
         if (STATS) {
 #pragma unroll
-            for (int k = 0; k < 6; k++) atomicAdd(&out.stats[1 + k], csum[k]);
+            for (int k = 0; k < 6; k++) atomicAdd(&out0.stats[1 + k], csum[k]);
         }
     }
 }
@@ -199,13 +208,56 @@ __global__ __launch_bounds__(256) void shrink_scatter_kernel(const int* in, int 
 }
 
 // ---- host-side launchers ------------------------------------------------------------------
-hipError_t launch_pass(const DevScene& sc, const DevConfig& cfg, const DevCamera& cam, const DevTiling& til,
-                       const DevOutput& out, int pass, int write_u8, int grid, bool stats, hipStream_t stream) {
-    const bool leaf1 = sc.leaf_size == 1;
-    if (leaf1 && !stats) hipLaunchKernelGGL((pass_kernel<true, false>), dim3(grid), dim3(PT_BLOCK), 0, stream, sc, cfg, cam, til, out, pass, write_u8);
-    else if (leaf1 && stats) hipLaunchKernelGGL((pass_kernel<true, true>), dim3(grid), dim3(PT_BLOCK), 0, stream, sc, cfg, cam, til, out, pass, write_u8);
-    else if (!leaf1 && !stats) hipLaunchKernelGGL((pass_kernel<false, false>), dim3(grid), dim3(PT_BLOCK), 0, stream, sc, cfg, cam, til, out, pass, write_u8);
-    else hipLaunchKernelGGL((pass_kernel<false, true>), dim3(grid), dim3(PT_BLOCK), 0, stream, sc, cfg, cam, til, out, pass, write_u8);
+int env_int(const char* name, int dflt, int lo, int hi) {
+    const char* e = getenv(name);
+    int v = e ? atoi(e) : dflt;
+    return v < lo ? lo : (v > hi ? hi : v);
+}
+
+using PassFn = void (*)(const LaunchParams*, int, int, int);
+
+static bool pass_prefetch() {
+    static int p = [] {
+        const char* e = getenv("PT_PREFETCH");
+        return e ? atoi(e) : 0;
+    }();
+    return p != 0;
+}
+
+static PassFn pass_fn(bool leaf1, bool stats, int minw) {
+    const bool pf = pass_prefetch();
+    if (leaf1 && !stats) {
+        if (pf) {
+            if (minw == 4) return pass_kernel<true, false, 4, true>;
+            if (minw == 6) return pass_kernel<true, false, 6, true>;
+            return pass_kernel<true, false, 5, true>;
+        }
+        if (minw == 4) return pass_kernel<true, false, 4, false>;
+        if (minw == 6) return pass_kernel<true, false, 6, false>;
+        return pass_kernel<true, false, 5, false>;
+    }
+    if (leaf1 && stats) return pass_kernel<true, true, 5, true>;
+    if (!stats) return pass_kernel<false, false, 5, true>;
+    return pass_kernel<false, true, 5, true>;
+}
+
+int pass_min_waves() {
+    static int w = [] {
+        const char* e = getenv("PT_MIN_WAVES");
+        int v = e ? atoi(e) : 6;
+        return (v == 4 || v == 5 || v == 6) ? v : 6;
+    }();
+    return w;
+}
+
+hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, int pass, int write_u8, int grid, bool stats,
+                       hipStream_t stream) {
+    PassFn fn = pass_fn(leaf1, stats, pass_min_waves());
+    const LaunchParams* a0 = params_dev;
+    int a1 = pass, a2 = write_u8, a3 = env_int("PT_CHUNK_MEGA", 0, 0, 4096);
+    void* args[] = {&a0, &a1, &a2, &a3};
+    hipError_t e = hipLaunchKernel((const void*)fn, dim3(grid), dim3(PT_BLOCK), args, 0, stream);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
@@ -221,8 +273,7 @@ int pass_grid_size(bool leaf1, bool stats) {
     int dev = 0, cus = 0, blocks = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* fn = leaf1 ? (stats ? (const void*)pass_kernel<true, true> : (const void*)pass_kernel<true, false>)
-                           : (stats ? (const void*)pass_kernel<false, true> : (const void*)pass_kernel<false, false>);
+    const void* fn = (const void*)pass_fn(leaf1, stats, pass_min_waves());
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, PT_BLOCK, 0) != hipSuccess || blocks <= 0) blocks = 4;
     if (cus <= 0) cus = 256;
     return cus * blocks;

@@ -272,7 +272,12 @@ PT_HD minstd minstd_seed(int32_t s) {
     return r;
 }
 PT_HD uint32_t minstd_next(minstd* e) {
-    e->x = (uint32_t)(((uint64_t)e->x * 48271ull) % 2147483647ull);
+    // x*48271 mod (2^31-1) by Mersenne folding: p < 2^47, (p & m) + (p >> 31) < 2^31 + 2^16,
+    // so one conditional subtraction gives exactly p % m without a 64-bit division.
+    const uint64_t p = (uint64_t)e->x * 48271ull;
+    uint32_t r = (uint32_t)(p & 2147483647ull) + (uint32_t)(p >> 31);
+    if (r >= 2147483647u) r -= 2147483647u;
+    e->x = r;
     return e->x;
 }
 // uniform_real_distribution<float>(a, b): ((float)(x - min) / (1 + (float)(max - min))) * (b - a) + a

@@ -15,7 +15,30 @@ namespace pt {
 #endif
 
 __device__ __forceinline__ v3 f4xyz(float4 a) { return mk3(a.x, a.y, a.z); }
+
+// Whole-record loads. Left alone, the compiler narrows a float4 load to the components used before
+// the next branch (dwordx3 for a box, then a dependent dword for next/slot after the test), which
+// puts a second L2 round trip on every node. The empty asm makes all four lanes live at once, so
+// each record is one global_load_dwordx4 and all loads of a record are in flight together.
+__device__ __forceinline__ float4 ld_record(const float4* p) {
+    float4 v = *p;
+    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+    return v;
+}
 __device__ __forceinline__ int f2i(float f) { return __float_as_int(f); }
+
+// Scene records through buffer descriptors: a raw_buffer_load_b128 is never narrowed by the
+// compiler and is only waited for at its first use, so a load can be issued early (prefetch).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int byte_offset) {
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_offset, 0, 0);
+    float4 f;
+    f.x = __uint_as_float(v.x); f.y = __uint_as_float(v.y); f.z = __uint_as_float(v.z); f.w = __uint_as_float(v.w);
+    return f;
+}
 
 // path_tracer_kernel.cu:46-52
 __device__ __forceinline__ v3 reflection(v3 n, v3 in) {
@@ -125,9 +148,19 @@ __device__ __forceinline__ float fresnel_conductor(v3 n, v3 in, float eta, float
     return (rs + rp) / 2.0f;
 }
 
+// pixels[i] / 255.0f for i in 0..255 (texture.h:47-66). Tabulated: the quotients are the same
+// correctly rounded values (constant-folded), and no multiply by 1/255 reproduces all 256 of them.
+struct U8Quotients {
+    float v[256];
+    constexpr U8Quotients() : v() {
+        for (int i = 0; i < 256; i++) v[i] = (float)i / 255.0f;
+    }
+};
+__device__ __constant__ const U8Quotients kU8 = U8Quotients();
+
 __device__ __forceinline__ v3 texel(const uint8_t* px, int idx) {
     uchar4 c = *reinterpret_cast<const uchar4*>(px + (size_t)idx * 4);
-    return mk3((int)c.x / 255.0f, (int)c.y / 255.0f, (int)c.z / 255.0f);
+    return mk3(kU8.v[c.x], kU8.v[c.y], kU8.v[c.z]);
 }
 
 // Core/texture.h:15-79 (also the face lookup of Core/cube_map.h:20-119, same arithmetic)
@@ -194,11 +227,7 @@ __device__ __forceinline__ bool sphere_t(float4 s, v3 o, v3 d, float* t_out) {
 }
 
 // Core/triangle.h:27-62 with edge1/edge2 precomputed (same IEEE subtraction, done once).
-__device__ __forceinline__ bool triangle_t(const float4* tg, int tri, v3 o, v3 d,
-                                           float* t, float* t1o, float* t2o) {
-    float4 a = tg[3 * tri + 0];
-    float4 b = tg[3 * tri + 1];
-    float4 c = tg[3 * tri + 2];
+__device__ __forceinline__ bool triangle_test(float4 a, float4 b, float4 c, v3 o, v3 d, float* t, float* t1o, float* t2o) {
     v3 v0 = f4xyz(a), e1 = f4xyz(b), e2 = f4xyz(c);
     v3 p = cross(d, e2);
     float det = dot(e1, p);
@@ -241,26 +270,39 @@ struct Counters {
 };
 
 // path_tracer_kernel.cu:85-161: stackless preorder walk with skip indices over one mesh.
-template <bool LEAF1, bool STATS>
+// PREFETCH: in preorder the node after a hit (or a leaf) is always pos+1, so its record is requested
+// while node pos is tested; a miss jumps to next_node_index and pays the full latency. The node
+// sequence, the tests and therefore the result are exactly the reference's.
+template <bool LEAF1, bool STATS, bool PREFETCH>
 __device__ __forceinline__ bool mesh_closest(const DevScene& sc, int begin, int end, v3 o, v3 d, v3 inv,
                                              float* ht, float* ht1, float* ht2, int* htri, Counters* ctr) {
+    const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
+    const __amdgpu_buffer_rsrc_t rt = make_rsrc(sc.tri_geom, sc.tri_count * 48);
     float min_t = __builtin_inff();
     float min_t1 = 0.0f, min_t2 = 0.0f;
     int min_tri = -1;
     bool hit = false;
     int pos = begin;
-    while (pos != end) {
-        float4 lo = sc.nodes[2 * pos + 0];
-        float4 hi = sc.nodes[2 * pos + 1];
+    if (pos == end) return false;
+    float4 lo = bload(rn, pos * 32), hi = bload(rn, pos * 32 + 16);
+    float4 nlo, nhi;
+    if (PREFETCH) { nlo = bload(rn, pos * 32 + 32); nhi = bload(rn, pos * 32 + 48); }
+    while (true) {
         if (STATS) ctr->nodes++;
         float entry;
         if (box_hit(lo, hi, o, inv, &entry) && entry <= min_t) {
-            int slot = f2i(hi.w);
+            const int slot = f2i(hi.w);
+            pos++;
+            if (PREFETCH) {
+                lo = nlo; hi = nhi;
+                if (pos != end) { nlo = bload(rn, pos * 32 + 32); nhi = bload(rn, pos * 32 + 48); }
+            }
             if (slot >= 0) {
                 if (LEAF1) {
                     float t, t1, t2;
                     if (STATS) ctr->tris++;
-                    if (triangle_t(sc.tri_geom, slot, o, d, &t, &t1, &t2) && t > 0.0f && t < min_t) {
+                    float4 a = bload(rt, slot * 48), b = bload(rt, slot * 48 + 16), c = bload(rt, slot * 48 + 32);
+                    if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < min_t) {
                         min_t = t; min_t1 = t1; min_t2 = t2; min_tri = slot; hit = true;
                     }
                 } else {
@@ -269,15 +311,20 @@ __device__ __forceinline__ bool mesh_closest(const DevScene& sc, int begin, int 
                         if (tri == -1) break;
                         float t, t1, t2;
                         if (STATS) ctr->tris++;
-                        if (triangle_t(sc.tri_geom, tri, o, d, &t, &t1, &t2) && t > 0.0f && t < min_t) {
+                        float4 a = bload(rt, tri * 48), b = bload(rt, tri * 48 + 16), c = bload(rt, tri * 48 + 32);
+                        if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < min_t) {
                             min_t = t; min_t1 = t1; min_t2 = t2; min_tri = tri; hit = true;
                         }
                     }
                 }
             }
-            pos++;
+            if (pos == end) break;
+            if (!PREFETCH) { lo = bload(rn, pos * 32); hi = bload(rn, pos * 32 + 16); }
         } else {
             pos = f2i(lo.w);
+            if (pos == end) break;
+            lo = bload(rn, pos * 32); hi = bload(rn, pos * 32 + 16);
+            if (PREFETCH) { nlo = bload(rn, pos * 32 + 32); nhi = bload(rn, pos * 32 + 48); }
         }
     }
     if (hit) { *ht = min_t; *ht1 = min_t1; *ht2 = min_t2; *htri = min_tri; }
@@ -285,23 +332,32 @@ __device__ __forceinline__ bool mesh_closest(const DevScene& sc, int begin, int 
 }
 
 // Per-path registers (the reference keeps these per pixel in HBM: rays, not_absorbed_colors,
-// accumulated_colors, scatterings; path_tracer_kernel.cu:275-297).
+// accumulated_colors, scatterings; path_tracer_kernel.cu:275-297). The scattering coefficients are
+// always either the configuration's air values or some material's medium (they are only ever copied
+// from out_medium, :594), so the path carries that material's id instead (-1 = air).
 struct PathState {
     v3 o, d;
     v3 thr;
     v3 rad;
-    float sa[3];
-    float ss[3];
+    int medium;
 };
+
+__device__ __forceinline__ void medium_coefficients(const DevScene& sc, const DevConfig& cfg, int medium, float sa[3],
+                                                    float ss[3]) {
+    if (medium < 0) {
+        for (int c = 0; c < 3; c++) { sa[c] = cfg.air_absorption[c]; ss[c] = cfg.air_reduced_scattering[c]; }
+    } else {
+        const DevMaterial& M = sc.materials[medium];
+        for (int c = 0; c < 3; c++) { sa[c] = M.absorption[c]; ss[c] = M.reduced_scattering[c]; }
+    }
+}
 
 // init_data_kernel + generate_ray_kernel for one pixel (path_tracer_kernel.cu:275-379).
 __device__ __forceinline__ void generate_path(const DevCamera& cam, const DevConfig& cfg, int pixel,
                                               int32_t hseed, PathState* ps) {
     ps->thr = mk3(1.0f, 1.0f, 1.0f);
     ps->rad = mk3(0.0f, 0.0f, 0.0f);
-    ps->sa[0] = cfg.air_absorption[0]; ps->sa[1] = cfg.air_absorption[1]; ps->sa[2] = cfg.air_absorption[2];
-    ps->ss[0] = cfg.air_reduced_scattering[0]; ps->ss[1] = cfg.air_reduced_scattering[1];
-    ps->ss[2] = cfg.air_reduced_scattering[2];
+    ps->medium = -1;
 
     int image_y = (int)((float)pixel / cam.res_x);
     int image_x = (int)((float)pixel - ((float)image_y * cam.res_x));
@@ -339,23 +395,22 @@ __device__ __forceinline__ void generate_path(const DevCamera& cam, const DevCon
     ps->d = normalize(image_plane - ap);
 }
 
-// One invocation of trace_ray_kernel for one live ray (path_tracer_kernel.cu:381-625).
-// Returns false when the reference would write -1 into energy_exist_pixels.
-template <bool LEAF1, bool STATS>
-__device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& cfg, int pixel, int depth,
-                                           int32_t hseed, PathState* ps, Counters* ctr) {
-    const v3 o = ps->o, d = ps->d;
-    minstd rng = minstd_seed(mul_wrap(mul_wrap(hseed, hash_pt(pixel)), hash_pt(depth)));
+// Closest hit over all spheres then every mesh BVH (path_tracer_kernel.cu:418-454).
+struct Hit {
+    float t, t1, t2;
+    int type;  // 0 none, 1 sphere, 2 triangle
+    int prim;
+};
 
-    float min_t = __builtin_inff();
-    float min_t1 = __builtin_inff(), min_t2 = __builtin_inff();
-    int type = 0;  // 0 none, 1 sphere, 2 triangle
-    int min_sphere = -1, min_tri = -1;
-
+template <bool LEAF1, bool STATS, bool PREFETCH>
+__device__ __forceinline__ Hit closest_hit(const DevScene& sc, v3 o, v3 d, Counters* ctr) {
+    Hit h;
+    h.t = __builtin_inff(); h.t1 = __builtin_inff(); h.t2 = __builtin_inff();
+    h.type = 0; h.prim = -1;
     for (int i = 0; i < sc.sphere_num; i++) {
         float t;
-        if (sphere_t(sc.spheres[2 * i], o, d, &t) && t < min_t && t > 0.0f) {
-            min_t = t; min_sphere = i; type = 1;
+        if (sphere_t(sc.spheres[2 * i], o, d, &t) && t < h.t && t > 0.0f) {
+            h.t = t; h.prim = i; h.type = 1;
         }
     }
     if (sc.mesh_num > 0) {
@@ -364,114 +419,136 @@ __device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& 
             int2 r = sc.mesh_range[m];
             float t, t1, t2;
             int tri;
-            if (mesh_closest<LEAF1, STATS>(sc, r.x, r.y, o, d, inv, &t, &t1, &t2, &tri, ctr) && t < min_t && t > 0.0f) {
-                min_t = t; min_t1 = t1; min_t2 = t2; min_tri = tri; type = 2;
+            if (mesh_closest<LEAF1, STATS, PREFETCH>(sc, r.x, r.y, o, d, inv, &t, &t1, &t2, &tri, ctr) && t < h.t && t > 0.0f) {
+                h.t = t; h.t1 = t1; h.t2 = t2; h.prim = tri; h.type = 2;
             }
         }
     }
+    return h;
+}
+
+template <bool STATS>
+__device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int pixel, int depth,
+                                          int32_t hseed, PathState* ps, const Hit& h, Counters* ctr);
+
+// One invocation of trace_ray_kernel for one live ray (path_tracer_kernel.cu:381-625).
+// Returns false when the reference would write -1 into energy_exist_pixels.
+template <bool LEAF1, bool STATS, bool PREFETCH>
+__device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& cfg, int pixel, int depth,
+                                           int32_t hseed, PathState* ps, Counters* ctr) {
+    const Hit h = closest_hit<LEAF1, STATS, PREFETCH>(sc, ps->o, ps->d, ctr);
+    return shade_hit<STATS>(sc, cfg, pixel, depth, hseed, ps, h, ctr);
+}
+
+// The part of trace_ray_kernel after the closest hit is known (:456-624): medium, material,
+// Fresnel-selected bounce, accumulation, kill test.
+template <bool STATS>
+__device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int pixel, int depth,
+                                          int32_t hseed, PathState* ps, const Hit& h, Counters* ctr) {
+    const v3 o = ps->o, d = ps->d;
+    const float min_t = h.t;
+    minstd rng = minstd_seed(mul_wrap(mul_wrap(hseed, hash_pt(pixel)), hash_pt(depth)));
 
     // medium: absorption and subsurface scattering (:456-492)
-    if (ps->ss[0] > 0.0f || length(mk3(ps->sa[0], ps->sa[1], ps->sa[2])) > cfg.sss_threshold) {
-        float r = minstd_uniform(&rng, 0.0f, 1.0f);
-        float dist = -log_pt(r) / ps->ss[0];
-        if (dist < min_t) {
-            float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
-            float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
-            ps->o = o + d * dist;
-            ps->d = sample_sphere(r1, r2);
-            ps->thr = ps->thr * absorption(ps->sa, dist);
-            if (STATS) ctr->scatter++;
-            return length(ps->thr) > cfg.energy_threshold;
+    {
+        float sa[3], ss[3];
+        medium_coefficients(sc, cfg, ps->medium, sa, ss);
+        if (ss[0] > 0.0f || length(mk3(sa[0], sa[1], sa[2])) > cfg.sss_threshold) {
+            float r = minstd_uniform(&rng, 0.0f, 1.0f);
+            float dist = -log_pt(r) / ss[0];
+            if (dist < min_t) {
+                float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
+                float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
+                ps->o = o + d * dist;
+                ps->d = sample_sphere(r1, r2);
+                ps->thr = ps->thr * absorption(sa, dist);
+                if (STATS) ctr->scatter++;
+                return length(ps->thr) > cfg.energy_threshold;
+            }
+            ps->thr = ps->thr * absorption(sa, min_t);
         }
-        ps->thr = ps->thr * absorption(ps->sa, min_t);
     }
 
-    if (STATS) { ctr->miss += type == 0; ctr->hit_sphere += type == 1; ctr->hit_mesh += type == 2; }
-    if (type == 0) {  // miss (:618-624)
+    if (STATS) { ctr->miss += h.type == 0; ctr->hit_sphere += h.type == 1; ctr->hit_mesh += h.type == 2; }
+    if (h.type == 0) {  // miss (:618-624)
         v3 bg = background(sc, cfg, d);
         ps->rad = ps->rad + ps->thr * bg;
         return false;
     }
 
-    DevMaterial mat;
-    v3 point, normal;
-    if (type == 1) {
-        float4 s = sc.spheres[2 * min_sphere];
-        int mid = f2i(sc.spheres[2 * min_sphere + 1].x);
-        mat = sc.materials[mid];
-        point = o + d * min_t;
+    // material of the hit (:496-527); fields are read where they are used
+    const v3 point = o + d * min_t;
+    v3 normal;
+    int mid;
+    v3 tex_d = mk3(1.0f, 1.0f, 1.0f), tex_s = mk3(1.0f, 1.0f, 1.0f);
+    bool has_tex_d = false, has_tex_s = false;
+    if (h.type == 1) {
+        float4 s = sc.spheres[2 * h.prim];
+        mid = f2i(sc.spheres[2 * h.prim + 1].x);
         normal = normalize(point - mk3(s.x, s.y, s.z));
     } else {
-        float4 s0 = sc.tri_shade[4 * min_tri + 0];
-        float4 s1 = sc.tri_shade[4 * min_tri + 1];
-        float4 s2 = sc.tri_shade[4 * min_tri + 2];
-        float4 s3 = sc.tri_shade[4 * min_tri + 3];
-        mat = sc.materials[f2i(s3.w)];
-        point = o + d * min_t;
+        const float4* sh = sc.tri_shade + 4 * h.prim;
+        float4 s0 = sh[0], s1 = sh[1], s2 = sh[2];
+        mid = f2i(sh[3].w);
         v3 n0 = mk3(s0.x, s0.y, s0.z), n1 = mk3(s0.w, s1.x, s1.y), n2 = mk3(s1.z, s1.w, s2.x);
-        float w = 1.0f - min_t1 - min_t2;
-        normal = n0 * w + n1 * min_t1 + n2 * min_t2;
-        if (mat.diffuse_texture_id != -1 || mat.specular_texture_id != -1) {
+        float w = 1.0f - h.t1 - h.t2;
+        normal = n0 * w + n1 * h.t1 + n2 * h.t2;
+        const DevMaterial& M = sc.materials[mid];
+        const int dt = M.diffuse_texture_id, st = M.specular_texture_id;
+        if (dt != -1 || st != -1) {
+            float4 s3 = sh[3];
             v2 uv0 = mk2(s2.y, s2.z), uv1 = mk2(s2.w, s3.x), uv2 = mk2(s3.y, s3.z);
-            v2 uv = uv0 * w + uv1 * min_t1 + uv2 * min_t2;
-            if (mat.diffuse_texture_id != -1) {
-                v3 tc = sample_texture(sc, mat.diffuse_texture_id, uv, cfg.use_bilinear);
-                mat.diffuse[0] = mat.diffuse[0] * tc.x;
-                mat.diffuse[1] = mat.diffuse[1] * tc.y;
-                mat.diffuse[2] = mat.diffuse[2] * tc.z;
-            }
-            if (mat.specular_texture_id != -1) {
-                v3 tc = sample_texture(sc, mat.specular_texture_id, uv, cfg.use_bilinear);
-                mat.specular[0] = mat.specular[0] * tc.x;
-                mat.specular[1] = mat.specular[1] * tc.y;
-                mat.specular[2] = mat.specular[2] * tc.z;
-            }
+            v2 uv = uv0 * w + uv1 * h.t1 + uv2 * h.t2;
+            if (dt != -1) { tex_d = sample_texture(sc, dt, uv, cfg.use_bilinear); has_tex_d = true; }
+            if (st != -1) { tex_s = sample_texture(sc, st, uv, cfg.use_bilinear); has_tex_s = true; }
         }
     }
+    const DevMaterial& M = sc.materials[mid];
 
     // media on either side of the surface (:529-547)
     float in_n = cfg.air_n;
-    float out_n = mat.refraction_index;
-    bool transparent = mat.is_transparent != 0;
-    float out_sa[3] = {mat.absorption[0], mat.absorption[1], mat.absorption[2]};
-    float out_ss[3] = {mat.reduced_scattering[0], mat.reduced_scattering[1], mat.reduced_scattering[2]};
+    float out_n = M.refraction_index;
+    const bool transparent = M.is_transparent != 0;
+    int out_medium = mid;
     if (dot(d, normal) > 0) {
         normal = normal * -1.0f;
         if (transparent) {
             float tn = in_n; in_n = out_n; out_n = tn;
-            for (int c = 0; c < 3; c++) {
-                out_sa[c] = cfg.air_absorption[c];
-                out_ss[c] = cfg.air_reduced_scattering[c];
-            }
+            out_medium = -1;
         }
     }
     v3 refr = refraction(normal, d, in_n, out_n);
     v3 bias_v = cfg.bias * normal;
 
     float R;
-    if (mat.extinction_coefficient == 0 || transparent) R = fresnel_dielectric(normal, d, in_n, out_n, refr);
-    else R = fresnel_conductor(normal, d, out_n, mat.extinction_coefficient);
+    const float k = M.extinction_coefficient;
+    if (k == 0 || transparent) R = fresnel_dielectric(normal, d, in_n, out_n, refr);
+    else R = fresnel_conductor(normal, d, out_n, k);
 
     float r = minstd_uniform(&rng, 0.0f, 1.0f);
     if (r < R) {  // reflection (:565-584)
         float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
         float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
-        float rough = pow_pt(mat.roughness, 1.85f) * 0.238f;
+        float rough = pow_pt(M.roughness, 1.85f) * 0.238f;
         v3 micro = sample_ggx(normal, rough, r1, r2);
         v3 mr = reflection(micro, d);
         float shadow = ggx_g1(rough, normal, micro, d) * ggx_g1(rough, normal, micro, mr);
+        v3 spec = mk3(M.specular[0], M.specular[1], M.specular[2]);
+        if (has_tex_s) spec = spec * tex_s;
         ps->o = point + bias_v;
         ps->d = mr;
-        ps->thr = ps->thr * (mk3(mat.specular[0], mat.specular[1], mat.specular[2]) * shadow);
+        ps->thr = ps->thr * (spec * shadow);
     } else if (transparent) {  // refraction (:585-596)
         ps->o = point - bias_v;
         ps->d = refr;
-        for (int c = 0; c < 3; c++) { ps->sa[c] = out_sa[c]; ps->ss[c] = out_ss[c]; }
+        ps->medium = out_medium;
         float ratio = out_n / in_n;
         ps->thr = ps->thr * (ratio * ratio);
     } else {  // diffuse (:597-610)
-        ps->rad = ps->rad + ps->thr * mk3(mat.emission[0], mat.emission[1], mat.emission[2]);
-        ps->thr = ps->thr * mk3(mat.diffuse[0], mat.diffuse[1], mat.diffuse[2]);
+        v3 diff = mk3(M.diffuse[0], M.diffuse[1], M.diffuse[2]);
+        if (has_tex_d) diff = diff * tex_d;
+        ps->rad = ps->rad + ps->thr * mk3(M.emission[0], M.emission[1], M.emission[2]);
+        ps->thr = ps->thr * diff;
         float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
         float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
         ps->o = point + bias_v;

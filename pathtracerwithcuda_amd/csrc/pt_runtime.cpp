@@ -6,6 +6,7 @@
 // one launch on a private HIP stream (pt_kernels.hip); the host never waits inside a frame.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -233,10 +234,17 @@ struct pt_context {
     // counters
     unsigned int* fetch = nullptr;
     unsigned long long* stats = nullptr;
+    LaunchParams* params = nullptr;  // device copy of the launch parameter block
     bool instrumented = false;
+    int schedule = -1;  // PT_SCHEDULE_*; -1: environment default (PT_MODE)
     int grid[2][2] = {{0, 0}, {0, 0}};
     std::vector<hipEvent_t> ev_start, ev_stop;
+    std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
     size_t ev_used = 0;
+    // wavefront schedule buffers (pt_wavefront.hip)
+    void* wave_mem = nullptr;
+    size_t wave_bytes = 0;
+    DevWave wave{};
     // thread_shrink scratch
     int* shrink_buf = nullptr;
     int* shrink_tiles = nullptr;
@@ -307,6 +315,8 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     s.sphere_num = (int)(st.spheres.size() / 2);
     s.leaf_size = st.leaf_size;
     s.cube_len = st.cube_len;
+    s.node_count = (int)(st.nodes.size() / 2);
+    s.tri_count = (int)(st.tri_geom.size() / 3);
     ctx->node_num = (int)(st.nodes.size() / 2);
     ctx->tri_num = (int)(st.tri_geom.size() / 3);
     ctx->has_scene = true;
@@ -363,6 +373,76 @@ int pass_grid(pt_context* ctx) {
     return g;
 }
 
+int ev_begin(pt_context* ctx, int kind) {
+    if (ctx->ev_used == ctx->ev_start.size()) {
+        hipEvent_t a, b;
+        PT_HIP(hipEventCreate(&a));
+        PT_HIP(hipEventCreate(&b));
+        ctx->ev_start.push_back(a);
+        ctx->ev_stop.push_back(b);
+        ctx->ev_kind.push_back(kind);
+    }
+    ctx->ev_kind[ctx->ev_used] = kind;
+    PT_HIP(hipEventRecord(ctx->ev_start[ctx->ev_used], ctx->stream));
+    return PT_OK;
+}
+
+int ev_end(pt_context* ctx) {
+    PT_HIP(hipEventRecord(ctx->ev_stop[ctx->ev_used], ctx->stream));
+    ctx->ev_used++;
+    return PT_OK;
+}
+
+// Queues for `units` rays and per-pixel state for the whole frame; append counters and work heads
+// for `depth` levels. Shard k of every queue holds at most the units of depth-0 region k
+// (pt_wavefront.hip shade_kernel), so seg_cap = ceil(units / PT_SHARDS) slots per shard suffice.
+size_t wave_counter_bytes(int depth) {
+    const size_t ncnt = (size_t)PT_SHARDS * (depth + 1);
+    const size_t cnt_bytes = (ncnt * sizeof(unsigned int) + 255) & ~(size_t)255;
+    return cnt_bytes + (size_t)2 * (depth > 0 ? depth : 1) * PT_HEAD_SET * sizeof(unsigned int);
+}
+
+int ensure_wave(pt_context* ctx, int units, int depth) {
+    const size_t px = (size_t)ctx->width * ctx->height;
+    const int seg_cap = units > 0 ? (units + PT_SHARDS - 1) / PT_SHARDS : 1;
+    const size_t slots = (size_t)PT_SHARDS * (size_t)seg_cap;
+    const size_t q = slots * sizeof(float4);
+    const size_t st = px * sizeof(float4);
+    size_t off[8], total = 0;
+    const size_t sizes[8] = {q, q, q, q, q, st, st, wave_counter_bytes(depth)};
+    for (int i = 0; i < 8; i++) { off[i] = total; total = (total + sizes[i] + 255) & ~(size_t)255; }
+    if (total > ctx->wave_bytes) {
+        if (ctx->wave_mem) (void)hipFree(ctx->wave_mem);
+        ctx->wave_mem = nullptr;
+        ctx->wave_bytes = 0;
+        PT_HIP(hipMalloc(&ctx->wave_mem, total));
+        ctx->wave_bytes = total;
+    }
+    uint8_t* b = (uint8_t*)ctx->wave_mem;
+    DevWave& w = ctx->wave;
+    w.q_o[0] = (float4*)(b + off[0]);
+    w.q_o[1] = (float4*)(b + off[1]);
+    w.q_d[0] = (float4*)(b + off[2]);
+    w.q_d[1] = (float4*)(b + off[3]);
+    w.hit = (float4*)(b + off[4]);
+    w.st_thr = (float4*)(b + off[5]);
+    w.st_rad = (float4*)(b + off[6]);
+    w.counters = (unsigned int*)(b + off[7]);
+    w.heads = w.counters + ((size_t)PT_SHARDS * (depth + 1) * sizeof(unsigned int) + 255) / 256 * 64;
+    w.seg_cap = seg_cap;
+    return PT_OK;
+}
+
+// PT_MODE=wave selects the extend/shade wavefront schedule; the default is the single persistent
+// pass kernel, measured faster on MI355X.
+bool use_wavefront() {
+    static int w = [] {
+        const char* e = getenv("PT_MODE");
+        return (e && std::strcmp(e, "wave") == 0) ? 1 : 0;
+    }();
+    return w != 0;
+}
+
 int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config, int first_pass,
                   int pass_count, int write_u8) {
     if (!ctx->has_scene) { set_error("no scene uploaded"); return PT_E_STATE; }
@@ -377,22 +457,48 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     out.image256 = ctx->image256;
     out.fetch = ctx->fetch;
     out.stats = ctx->stats;
+    LaunchParams lp;
+    lp.sc = ctx->scene;
+    lp.cfg = dc;
+    lp.cam = dcam;
+    lp.til = ctx->tiling;
+    lp.out = out;
+    const int D = dc.max_depth > 0 ? dc.max_depth : 0;
+    if (ctx->schedule == PT_SCHEDULE_WAVEFRONT || (ctx->schedule < 0 && use_wavefront())) {
+        int rc = ensure_wave(ctx, ctx->tiling.unit_count, D);
+        if (rc != PT_OK) return rc;
+        lp.wave = ctx->wave;
+        PT_HIP(hipMemcpyAsync(ctx->params, &lp, sizeof(lp), hipMemcpyHostToDevice, ctx->stream));
+        const bool leaf1 = ctx->scene.leaf_size == 1;
+        const bool st = ctx->instrumented;
+        for (int i = 0; i < pass_count; i++) {
+            const int pass = first_pass + i;
+            const int w8 = write_u8 == 1 || (write_u8 == 2 && i == pass_count - 1);
+            PT_HIP(hipMemsetAsync(ctx->wave.counters, 0, wave_counter_bytes(D), ctx->stream));
+            for (int d = 0; d < D; d++) {
+                if ((rc = ev_begin(ctx, 1)) != PT_OK) return rc;
+                PT_HIP(launch_extend(ctx->params, d == 0, leaf1, st, d, pass, ctx->stream));
+                if ((rc = ev_end(ctx)) != PT_OK) return rc;
+                if ((rc = ev_begin(ctx, 2)) != PT_OK) return rc;
+                PT_HIP(launch_shade(ctx->params, d == 0, d == D - 1, st, d, pass, ctx->stream));
+                if ((rc = ev_end(ctx)) != PT_OK) return rc;
+            }
+            if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;
+            PT_HIP(launch_finalize(ctx->params, ctx->tiling.unit_count, pass, w8, D > 0, ctx->stream));
+            if ((rc = ev_end(ctx)) != PT_OK) return rc;
+        }
+        return PT_OK;
+    }
     const int grid = pass_grid(ctx);
+    PT_HIP(hipMemcpyAsync(ctx->params, &lp, sizeof(lp), hipMemcpyHostToDevice, ctx->stream));
     for (int i = 0; i < pass_count; i++) {
         int pass = first_pass + i;
         int w8 = write_u8 == 1 || (write_u8 == 2 && i == pass_count - 1);
-        PT_HIP(hipMemsetAsync(ctx->fetch, 0, sizeof(unsigned int), ctx->stream));
-        if (ctx->ev_used == ctx->ev_start.size()) {
-            hipEvent_t a, b;
-            PT_HIP(hipEventCreate(&a));
-            PT_HIP(hipEventCreate(&b));
-            ctx->ev_start.push_back(a);
-            ctx->ev_stop.push_back(b);
-        }
-        PT_HIP(hipEventRecord(ctx->ev_start[ctx->ev_used], ctx->stream));
-        PT_HIP(launch_pass(ctx->scene, dc, dcam, ctx->tiling, out, pass, w8, grid, ctx->instrumented, ctx->stream));
-        PT_HIP(hipEventRecord(ctx->ev_stop[ctx->ev_used], ctx->stream));
-        ctx->ev_used++;
+        PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
+        int rc = ev_begin(ctx, 0);
+        if (rc != PT_OK) return rc;
+        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, pass, w8, grid, ctx->instrumented, ctx->stream));
+        if ((rc = ev_end(ctx)) != PT_OK) return rc;
     }
     return PT_OK;
 }
@@ -446,8 +552,9 @@ extern "C" int pt_context_create(int device, pt_context** out) {
     ctx->device = device;
     int rc = ensure_device(ctx);
     if (rc == PT_OK && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { set_error("stream"); rc = PT_E_HIP; }
-    if (rc == PT_OK && hipMalloc(&ctx->fetch, 256) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
+    if (rc == PT_OK && hipMalloc(&ctx->fetch, PT_HEAD_SET * sizeof(unsigned int)) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
     if (rc == PT_OK && hipMalloc(&ctx->stats, 256) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
+    if (rc == PT_OK && hipMalloc(&ctx->params, sizeof(LaunchParams)) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
     if (rc == PT_OK && hipMemset(ctx->stats, 0, 256) != hipSuccess) { set_error("memset"); rc = PT_E_HIP; }
     if (rc != PT_OK) { pt_context_destroy(ctx); return rc; }
     *out = ctx;
@@ -463,6 +570,8 @@ extern "C" void pt_context_destroy(pt_context* ctx) {
     if (ctx->image256) (void)hipFree(ctx->image256);
     if (ctx->fetch) (void)hipFree(ctx->fetch);
     if (ctx->stats) (void)hipFree(ctx->stats);
+    if (ctx->params) (void)hipFree(ctx->params);
+    if (ctx->wave_mem) (void)hipFree(ctx->wave_mem);
     if (ctx->shrink_buf) (void)hipFree(ctx->shrink_buf);
     if (ctx->shrink_tiles) (void)hipFree(ctx->shrink_tiles);
     if (ctx->shrink_total) (void)hipFree(ctx->shrink_total);
@@ -577,9 +686,40 @@ extern "C" int pt_stats(pt_context* ctx, unsigned long long* segments, unsigned 
     return PT_OK;
 }
 
+extern "C" int pt_set_schedule(pt_context* ctx, int schedule) {
+    if (!ctx) { set_error("null context"); return PT_E_ARG; }
+    if (schedule < -1 || schedule > PT_SCHEDULE_WAVEFRONT) { set_error("unknown schedule %d", schedule); return PT_E_ARG; }
+    ctx->schedule = schedule;
+    return PT_OK;
+}
+
+extern "C" int pt_get_schedule(pt_context* ctx) {
+    if (!ctx) { set_error("null context"); return PT_E_ARG; }
+    if (ctx->schedule >= 0) return ctx->schedule;
+    return use_wavefront() ? PT_SCHEDULE_WAVEFRONT : PT_SCHEDULE_PERSISTENT;
+}
+
 extern "C" int pt_set_instrumented(pt_context* ctx, int on) {
     if (!ctx) return PT_E_ARG;
     ctx->instrumented = on != 0;
+    return PT_OK;
+}
+
+extern "C" int pt_kernel_time_kind(pt_context* ctx, int kind, double* total_ms, int* launches) {
+    if (!ctx) return PT_E_ARG;
+    PT_HIP(hipSetDevice(ctx->device));
+    double t = 0.0;
+    int n = 0;
+    for (size_t i = 0; i < ctx->ev_used; i++) {
+        if (kind >= 0 && ctx->ev_kind[i] != kind) continue;
+        PT_HIP(hipEventSynchronize(ctx->ev_stop[i]));
+        float ms = 0.0f;
+        PT_HIP(hipEventElapsedTime(&ms, ctx->ev_start[i], ctx->ev_stop[i]));
+        t += ms;
+        n++;
+    }
+    if (total_ms) *total_ms = t;
+    if (launches) *launches = n;
     return PT_OK;
 }
 

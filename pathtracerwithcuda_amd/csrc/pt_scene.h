@@ -63,6 +63,8 @@ struct DevScene {
     int sphere_num;
     int leaf_size;
     int cube_len;
+    int node_count;  // records in `nodes` (2 float4 each); bounds of the node buffer descriptor
+    int tri_count;   // records in `tri_geom` (3 float4 each)
 };
 
 // The subset of Core/configuration.h:9-34 that the kernel reads.
@@ -109,8 +111,40 @@ struct DevTiling {
 struct DevOutput {
     float* image;            // float3 running sum, reference layout (12 B stride)
     uint8_t* image256;       // uchar3 (3 B stride), may be null
-    unsigned int* fetch;     // work counter (zeroed before launch)
+    unsigned int* fetch;     // PT_HEAD_SET work heads of the single-kernel pass (zeroed before launch)
     unsigned long long* stats;  // [0] ray segments, [1..] optional instrumentation
+};
+
+// Wavefront queues (pt_wavefront.hip). Ray slots are dense per depth; path state is per pixel.
+//   q_o[k][s]  {origin.xyz, pixel (int bits)}     q_d[k][s] {direction.xyz, -}      (k = depth & 1)
+//   hit[s]     {t, t1, t2, prim << 2 | type}       type 0 none, 1 sphere, 2 triangle
+//   st_thr[px] {throughput.xyz, medium id bits}    st_rad[px] {radiance.xyz, -}
+//   counters   [d * PT_SHARDS + k]: rays appended to shard k of the depth-d queue (d >= 1); shard k
+//              occupies slots [k * seg_cap, k * seg_cap + count). Depth 0: slot == unit, the units
+//              cut into PT_SHARDS regions of seg_cap = ceil(units / PT_SHARDS).
+//   heads      PT_HEAD_SET uints per launch of a pass (extend d: 2d, shade d: 2d + 1), pt_work.h
+#define PT_SHARDS 8
+struct DevWave {
+    float4* q_o[2];
+    float4* q_d[2];
+    float4* hit;       // indexed by the dense ray index of the depth
+    float4* st_thr;
+    float4* st_rad;
+    unsigned int* counters;
+    unsigned int* heads;
+    int seg_cap;
+    int pad;
+};
+
+// Everything a pass launch reads, in one device-resident block (pt_runtime.cpp uploads it once per
+// render call; kernels take its address as their only pointer argument).
+struct LaunchParams {
+    DevScene sc;
+    DevConfig cfg;
+    DevCamera cam;
+    DevTiling til;
+    DevOutput out;
+    DevWave wave;
 };
 
 }  // namespace pt

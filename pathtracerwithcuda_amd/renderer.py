@@ -115,6 +115,18 @@ class Renderer:
         keys = ("segments", "nodes", "tris", "hit_mesh", "hit_sphere", "miss", "scatter")
         return dict(zip(keys, (int(x) for x in a)))
 
+    SCHEDULES = {"persistent": 0, "wavefront": 1}
+
+    def set_schedule(self, schedule: str | None) -> None:
+        """'persistent' (one launch per pass), 'wavefront' (extend + shade per depth) or None (default)."""
+        check(self._lib.pt_set_schedule(self._ctx, -1 if schedule is None else self.SCHEDULES[schedule]),
+              "pt_set_schedule")
+
+    def schedule(self) -> str:
+        v = self._lib.pt_get_schedule(self._ctx)
+        check(min(v, 0), "pt_get_schedule")
+        return {0: "persistent", 1: "wavefront"}[v]
+
     def set_instrumented(self, on: bool) -> None:
         check(self._lib.pt_set_instrumented(self._ctx, 1 if on else 0), "pt_set_instrumented")
 
@@ -124,6 +136,12 @@ class Renderer:
         check(self._lib.pt_math_eval_device(self._ctx, which, x.ctypes.data, len(x), o0.ctypes.data, o1.ctypes.data),
               "pt_math_eval_device")
         return o0, o1
+
+    def kernel_time_kind(self, kind: int) -> tuple[float, int]:
+        """kind: 0 single-kernel pass, 1 extend (BVH walk), 2 shade, 3 finalize, -1 all."""
+        ms, n = C.c_double(), C.c_int()
+        check(self._lib.pt_kernel_time_kind(self._ctx, kind, C.byref(ms), C.byref(n)), "pt_kernel_time_kind")
+        return ms.value, n.value
 
     def kernel_time(self) -> tuple[float, int]:
         ms, n = C.c_double(), C.c_int()

@@ -35,9 +35,12 @@ def assert_bitwise(gpu, ref, what=""):
                              f"max |d| {np.nanmax(d):.3g}, mean |d| {np.nanmean(d):.3g}")
 
 
-@pytest.fixture(scope="module")
-def gpu(require_gpu):
+@pytest.fixture(scope="module", params=["persistent", "wavefront"])
+def gpu(require_gpu, request):
+    """Every parity test runs under both kernel schedules (pt_set_schedule): they must agree bitwise."""
     r = pt.Renderer(0)
+    r.set_schedule(request.param)
+    assert r.schedule() == request.param
     yield r
     r.close()
 

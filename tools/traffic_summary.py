@@ -1,0 +1,56 @@
+"""Per-kernel HBM traffic from two separate rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+    python tools/traffic_summary.py gpurun_out/<tag> profiles/<round> [--workload KEY --kernel SUBSTR]
+
+Writes <out>/pmc_summary.json (mean KB per dispatch per kernel) and, with --workload, records the
+dominant kernel's per-launch HBM bytes in profiles/traffic.json (read by bench.py as roofline.traffic).
+Corrections per MI355X_MICROARCH.md §HBM: counters are in KB (x1024); on gfx950 FETCH_SIZE reports
+half the bytes of 16-B-per-lane reads, so it is doubled; WRITE_SIZE is taken as is.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+
+ap = argparse.ArgumentParser()
+ap.add_argument("src")
+ap.add_argument("out")
+ap.add_argument("--workload", default=None)
+ap.add_argument("--kernel", default="pass_kernel<true, false, 6")
+ap.add_argument("--round", default=None)
+args = ap.parse_args()
+
+agg = {}
+for sub, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+    for f in glob.glob(os.path.join(args.src, sub, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = r["Kernel_Name"].split("(")[0]
+            agg.setdefault(k, {}).setdefault(counter, []).append(float(r["Counter_Value"]))
+
+summary = {k: {c: {"dispatches": len(v), "mean_kb": sum(v) / len(v)} for c, v in d.items()} for k, d in agg.items()}
+os.makedirs(args.out, exist_ok=True)
+json.dump(summary, open(os.path.join(args.out, "pmc_summary.json"), "w"), indent=1)
+
+if args.workload:
+    hits = [k for k in summary if args.kernel in k]
+    if len(hits) != 1:
+        raise SystemExit(f"kernel {args.kernel!r} matched {hits}")
+    k = hits[0]
+    fetch = summary[k]["FETCH_SIZE"]["mean_kb"] * 1024 * 2
+    write = summary[k]["WRITE_SIZE"]["mean_kb"] * 1024
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
+    d = json.load(open(path)) if os.path.exists(path) else {}
+    d[args.workload] = {
+        "hbm_bytes_per_launch": round(fetch + write),
+        "fetch_bytes": round(fetch),
+        "write_bytes": round(write),
+        "source": f"{os.path.relpath(args.out)}/pmc_summary.json (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
+                  "separate passes; FETCH_SIZE x2 gfx950 correction, KB x1024)",
+        "kernel": k,
+        "round": args.round or os.path.basename(os.path.normpath(args.out)),
+    }
+    json.dump(d, open(path, "w"), indent=1)
+    print(k, d[args.workload])
