@@ -116,23 +116,11 @@ def main() -> int:
     cfg = pt.configuration(max_tracer_depth=DEPTH)
     cam = pt.camera(WIDTH, HEIGHT, **CAMERA)
     r.upload(scene, cfg)
-    image = None
-    if world > 1:
-        image = torch.zeros(WIDTH * HEIGHT * 3, dtype=torch.float32, device=f"cuda:{local}")
-        r.setup_frame(WIDTH, HEIGHT, image.data_ptr())
-        r.set_tiling(BAND_ROWS, world, rank)
-    else:
-        r.setup_frame(WIDTH, HEIGHT)
+    tiled = pt.TiledFrame(r, WIDTH, HEIGHT, dist if world > 1 else None, BAND_ROWS,
+                          device=f"cuda:{local}" if world > 1 else None)
 
     def frame():
-        r.render(cam, cfg, 1, SPP, write_u8=2 if world == 1 else 0)
-        if world > 1:
-            r.synchronize()
-            dist.reduce(image, dst=0)  # RCCL over xGMI: the one collective of the frame
-            if rank == 0:
-                torch.cuda.synchronize()
-                r.finalize_u8(cfg, SPP)
-        r.synchronize()
+        tiled.render(cam, cfg, SPP)
 
     # roofline inputs: one instrumented (untimed) frame for the visit counts
     r.set_instrumented(True)

@@ -15,6 +15,12 @@
  *   math OR_MATH_CEPHES / OR_MATH_LIBM (oracle_math.h).
  * Scene input is the reference's own data layout (include/pt_types.h): triangle.mat and
  * bvh_node_device.triangle_indices are dereferenced exactly as the reference does.
+ *
+ * PINNING: the reference ships no tests, golden images or known-answer vectors, and its sources
+ * cannot be compiled here without stand-in headers (CUDA runtime, FreeImage, backslash includes),
+ * so oracle/_ref is not built. Pinned: the RNG streams and hash (rocThrust golden vectors,
+ * tests/golden/rng_thrust.json). The full-path restatement is PARITY UNPINNED against reference
+ * output; each function cites the reference file:line it follows.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -606,6 +612,13 @@ int or_render(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangle* t
     if (stats) { stats[0] = segs; stats[1] = nodes; stats[2] = tris; }
     free(st.alive); free(st.rays); free(st.thr); free(st.rad); free(st.sca);
     return 0;
+}
+
+/* The 8-bit gamma output of a float running sum of `pass` passes, for n pixels (used to check the
+ * multi-rank finalize after a reduce). */
+void or_gamma_u8(const pt_configuration* cfg, const float* image, int n, int pass, int math_mode,
+                 unsigned char* image256) {
+    for (int k = 0; k < n; k++) gamma_u8(math_mode, cfg, image + (size_t)k * 3, pass, image256 + (size_t)k * 3);
 }
 
 /* Math known-answer exports (tests/test_oracle_math.py). */

@@ -41,6 +41,8 @@ def lib() -> C.CDLL:
         h.or_rng_stream.argtypes = [C.c_int, C.c_int32, C.c_int, C.c_float, C.c_float, C.c_void_p]
         h.or_hash.restype = C.c_int32
         h.or_hash.argtypes = [C.c_int32]
+        h.or_gamma_u8.restype = None
+        h.or_gamma_u8.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         h.or_math_eval.restype = None
         h.or_math_eval.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         _lib = h
@@ -70,6 +72,14 @@ def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.
     if rc != 0:
         raise MemoryError("oracle allocation failed")
     return img, img8, {"segments": stats[0], "nodes": stats[1], "tris": stats[2]}
+
+
+def gamma_u8(cfg, image: np.ndarray, pass_: int, math: str = "cephes") -> np.ndarray:
+    """pixel_256_transform_gamma_corrected of a float running sum of `pass_` passes."""
+    img = np.ascontiguousarray(image, np.float32).reshape(-1, 3)
+    out = np.zeros(img.shape, np.uint8)
+    lib().or_gamma_u8(C.addressof(cfg), img.ctypes.data, len(img), pass_, MATH[math], out.ctypes.data)
+    return out
 
 
 def rng_stream(kind: str, seed: int, n: int, a: float = 0.0, b: float = 1.0) -> np.ndarray:

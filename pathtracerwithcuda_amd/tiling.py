@@ -1,0 +1,67 @@
+"""Frame tiling across ranks and the one-collective frame of the multi-GPU path.
+
+Every pixel's path depends only on (pass, global pixel index, depth) and the read-only scene
+(path_tracer_kernel.cu:324,415), so a frame shards with no exchange while rendering. Rank r of N
+owns the rows y with (y // band_rows) % N == r: interleaved bands balance sky against mesh. Each
+rank renders all passes of its rows into a full-size float accumulation buffer that is zero
+elsewhere, one reduce (RCCL over xGMI on the GPU box; any torch.distributed backend here) sums the
+buffers on rank 0, which then writes the 8-bit gamma image. Summing zeros is exact, so the result
+is bit-identical to one GPU.
+
+The renderer is anything with the pathtracerwithcuda_amd.Renderer frame interface (setup_frame,
+set_tiling, render, synchronize, finalize_u8); tests/test_multirank.py drives this same code
+with gloo on the CPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def owned_rows(height: int, band_rows: int, band_count: int, band_index: int) -> np.ndarray:
+    """Rows owned by one rank (DevTiling, csrc/pt_scene.h)."""
+    y = np.arange(height)
+    return y[(y // band_rows) % band_count == band_index]
+
+
+def owned_pixels(width: int, height: int, band_rows: int, band_count: int, band_index: int) -> np.ndarray:
+    """Pixel indices owned by one rank, in the kernel's unit order (unit_to_pixel, csrc/pt_work.h)."""
+    rows = owned_rows(height, band_rows, band_count, band_index)
+    return (rows[:, None] * width + np.arange(width)[None, :]).reshape(-1).astype(np.int32)
+
+
+class TiledFrame:
+    """One frame of `spp` passes on this rank's bands, reduced to rank 0 (world > 1)."""
+
+    def __init__(self, renderer, width: int, height: int, dist=None, band_rows: int = 8, device=None):
+        self.r = renderer
+        self.width, self.height = width, height
+        self.dist = dist if (dist is not None and dist.is_available() and dist.is_initialized()) else None
+        self.world = self.dist.get_world_size() if self.dist else 1
+        self.rank = self.dist.get_rank() if self.dist else 0
+        self.band_rows = band_rows
+        self.image = None
+        if self.world > 1:
+            import torch
+
+            self.image = torch.zeros(width * height * 3, dtype=torch.float32, device=device)
+            renderer.setup_frame(width, height, self.image.data_ptr())
+            renderer.set_tiling(band_rows, self.world, self.rank)
+        else:
+            renderer.setup_frame(width, height)
+
+    def _device_sync(self) -> None:
+        if self.image is not None and self.image.is_cuda:
+            import torch
+
+            torch.cuda.synchronize(self.image.device)
+
+    def render(self, cam, cfg, spp: int) -> None:
+        """Passes 1..spp; rank 0 ends with the full float image and its 8-bit output."""
+        self.r.render(cam, cfg, 1, spp, write_u8=2 if self.world == 1 else 0)
+        if self.world > 1:
+            self.r.synchronize()
+            self.dist.reduce(self.image, dst=0)  # the one collective of the frame
+            if self.rank == 0:
+                self._device_sync()
+                self.r.finalize_u8(cfg, spp)
+        self.r.synchronize()

@@ -1,0 +1,116 @@
+"""Multi-rank frame logic on the CPU: world_size 2 over gloo, through the same TiledFrame that
+bench.py uses on the GPU box (band ownership, per-rank render, reduce to rank 0, 8-bit finalize).
+
+The per-rank renderer here is a CPU stand-in with the Renderer frame interface, backed by the
+oracle (test infrastructure). The HIP kernels' band tiling is covered on the GPU by
+tests/test_gpu_parity.py::test_band_tiling_partitions_the_frame. The bar is the same as one GPU:
+the reduced float image and its 8-bit output must equal a single full-frame render bitwise.
+"""
+import ctypes as C
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+import pathtracerwithcuda_amd as pt
+
+W, H, SPP, BAND = 40, 27, 2, 4
+
+
+class OracleFrameRenderer:
+    """CPU stand-in for pathtracerwithcuda_amd.Renderer's frame interface."""
+
+    def __init__(self, scene):
+        self.scene = scene
+        self.tiling = (1, 1, 0)
+
+    def setup_frame(self, width, height, image_ptr=None):
+        self.w, self.h = width, height
+        n = width * height
+        if image_ptr:
+            self.img = np.ctypeslib.as_array((C.c_float * (n * 3)).from_address(image_ptr)).reshape(n, 3)
+        else:
+            self.img = np.zeros((n, 3), np.float32)
+        self.img8 = np.zeros((n, 3), np.uint8)
+
+    def set_tiling(self, band_rows, band_count, band_index):
+        self.tiling = (band_rows, band_count, band_index)
+
+    def render(self, cam, cfg, first_pass, pass_count, write_u8=0):
+        assert first_pass == 1  # pass 1 overwrites: the owned pixels receive the whole sum
+        px = pt.owned_pixels(self.w, self.h, *self.tiling)
+        img, img8, _ = oracle.render(self.scene.view, cam, cfg, first_pass, pass_count, pixels=px)
+        self.img[px] = img
+        if write_u8:
+            self.img8[px] = img8
+
+    def synchronize(self):
+        pass
+
+    def finalize_u8(self, cfg, pass_):
+        self.img8[:] = oracle.gamma_u8(cfg, self.img, pass_)
+
+
+def _scene():
+    return pt.cornell_scene(pt.torus_knot(40, 12), cube_length=16)
+
+
+def _setup():
+    cfg = pt.configuration(max_tracer_depth=5)
+    cam = pt.camera(W, H, pitch=0.08, radius=12.5, center=(0, 1.2, 0))
+    return cfg, cam
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        scene = _scene()
+        cfg, cam = _setup()
+        r = OracleFrameRenderer(scene)
+        frame = pt.TiledFrame(r, W, H, dist, BAND, device="cpu")
+        assert frame.world == world and frame.rank == rank
+        frame.render(cam, cfg, SPP)
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), img=r.img.copy(), img8=r.img8.copy(),
+                 owned=pt.owned_pixels(W, H, BAND, world, rank))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_owned_pixels_partition_the_frame():
+    for world in (1, 2, 3, 8):
+        parts = [pt.owned_pixels(W, H, BAND, world, k) for k in range(world)]
+        allpx = np.concatenate(parts)
+        assert np.array_equal(np.sort(allpx), np.arange(W * H))
+        for k, p in enumerate(parts):
+            rows = np.unique(p // W)
+            assert np.array_equal(rows, pt.owned_rows(H, BAND, world, k))
+            assert all((y // BAND) % world == k for y in rows)
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_tiled_frame_equals_single_render(tmp_path):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    r0 = np.load(tmp_path / "rank0.npz")
+    r1 = np.load(tmp_path / "rank1.npz")
+    cfg, cam = _setup()
+    scene = _scene()  # keep alive: the view points into it
+    ref, ref8, _ = oracle.render(scene.view, cam, cfg, 1, SPP)
+    # rank 0 holds the reduced frame and its 8-bit image
+    assert np.array_equal(r0["img"].view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(r0["img8"], ref8)
+    # the two ranks' bands are disjoint and cover the frame (non-root buffers are scratch after a reduce)
+    assert not np.intersect1d(r0["owned"], r1["owned"]).size
+    assert len(r0["owned"]) + len(r1["owned"]) == W * H
