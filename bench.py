@@ -2,8 +2,8 @@
 """Benchmark of the radiance loop: Mrays/s and ms/frame at 1920x1080, 8 spp, 8 bounces on the
 Cornell + OBJ-mesh scene (BASELINE.json `metric`), on 1 GPU or tiled across N GPUs of one node.
 
-A step is one frame: 8 passes (one persistent HIP launch each) over the 1920x1080 frame and the
-8-bit gamma output; with N > 1 each rank renders its interleaved 8-row bands and the float
+A step is one frame: 8 passes (batched into one persistent HIP launch plus an in-order accumulate)
+over the 1920x1080 frame and the 8-bit gamma output; with N > 1 each rank renders its interleaved 8-row bands and the float
 accumulation buffer is summed to rank 0 with one RCCL reduce (torch.distributed "nccl"), after
 which rank 0 writes the 8-bit image. Mrays/s = ray segments traced (the live-ray counts the
 reference's thread_shrink returns, summed over passes and depths and over ranks) / wall time.
@@ -171,14 +171,15 @@ def main() -> int:
     value = segments / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1000.0
     avg_launch_s = kernel_ms / max(launches, 1) / 1000.0
+    launches_per_frame = launches / max(args.steps, 1)
     if schedule == "persistent":
-        # one launch = one pass over the frame (this rank's bands when tiled)
+        # one launch = a batch of passes over the frame (this rank's bands when tiled)
         bytes_per_launch = algorithmic_bytes(counts, scene.view.sphere_num, cfg.bvh_leaf_node_triangle_num,
-                                             WIDTH * HEIGHT, SPP) / SPP / world
+                                             WIDTH * HEIGHT, SPP) / world / launches_per_frame
         kernel_name = "pass_kernel<LEAF1=true,STATS=false,MINW=6>"
     else:
-        # one launch = one depth of one pass; averaged over the SPP * DEPTH extend launches
-        bytes_per_launch = extend_bytes(counts, scene.view.sphere_num) / (SPP * DEPTH) / world
+        # one launch = one depth of one pass
+        bytes_per_launch = extend_bytes(counts, scene.view.sphere_num) / world / launches_per_frame
         kernel_name = "extend_kernel<LEAF1=true,STATS=false>"
     achieved = bytes_per_launch / avg_launch_s / 1e9
     workload = f"cornell+knot{KNOT[0] * KNOT[1] * 2}_{WIDTH}x{HEIGHT}_spp{SPP}_d{DEPTH}"
@@ -217,6 +218,7 @@ def main() -> int:
             "traffic": traffic,
             "kernel": kernel_name,
             "avg_launch_ms": round(avg_launch_s * 1000, 4),
+            "launches_per_frame": round(launches_per_frame, 3),
             "algorithmic_bytes_per_launch": round(bytes_per_launch),
             "counts_per_frame": counts,
         },

@@ -10,8 +10,10 @@
 
 namespace pt {
 
-hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, int pass, int write_u8, int grid, bool stats,
-                       hipStream_t stream);
+hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, int first_pass, int batch_log2, int write_u8,
+                       int grid, bool stats, hipStream_t stream);
+hipError_t launch_accumulate(const LaunchParams* params_dev, int units, int first_pass, int batch_log2, int write_u8,
+                             hipStream_t stream);
 hipError_t launch_extend(const LaunchParams* P, bool gen, bool leaf1, bool stats, int depth, int pass, hipStream_t s);
 hipError_t launch_shade(const LaunchParams* P, bool first, bool last, bool stats, int depth, int pass, hipStream_t s);
 int shade_grid_waves();

@@ -19,11 +19,18 @@
 
 namespace pt {
 
-// MINW = minimum waves per SIMD requested from the register allocator (0: compiler's choice);
-// the persistent loop is latency-bound, so occupancy is the first-order knob.
+// MINW = minimum waves per SIMD requested from the register allocator; the persistent loop is
+// latency-bound, so occupancy is the first-order knob.
+//
+// One launch renders 2^batch_log2 consecutive passes (first_pass ...). Work unit u is pass
+// first_pass + (u & (B-1)) of local pixel u >> batch_log2: the passes of one pixel sit in adjacent
+// lanes, so their primary rays (same pixel, different jitter) walk the same BVH nodes together.
+// With B == 1 a finished path accumulates into the image directly; with B > 1 it stores its clamped
+// radiance in pass_rad[u] and accumulate_kernel sums the passes in pass order afterwards, so the
+// running sum is bit-identical to one launch per pass.
 template <bool LEAF1, bool STATS, int MINW, bool PREFETCH>
-__global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams* __restrict__ params, int pass,
-                                                              int write_u8, int chunk) {
+__global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams* __restrict__ params, int first_pass,
+                                                              int write_u8, int chunk, int batch_log2) {
     const int lane = threadIdx.x & 63;
     // The launch parameters live in device memory and are re-read (scalar loads, K$ hits) inside
     // every iteration instead of being pinned in SGPRs for the whole kernel: the empty asm makes
@@ -31,20 +38,20 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
     const LaunchParams* P0 = params;
     const DevConfig& cfg0 = P0->cfg;
     const DevOutput& out0 = P0->out;
-    const int32_t hseed = hash_pt(pass);
     const float clamp_hi = (float)cfg0.max_depth * 2.0f;
     const unsigned long long lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
     PathState ps;
-    int pixel = -1;
+    unsigned int unit = 0;
+    int32_t pseed = 0;
     int depth = 0;
     bool need = true;   // lane wants a new path
-    bool done = false;  // work counter exhausted for this lane
+    bool done = false;  // no work left for this lane
     unsigned long long segments = 0;
     Counters ctr = {0u, 0u, 0u, 0u, 0u, 0u};
     unsigned long long csum[6] = {0, 0, 0, 0, 0, 0};
-    // pixels in PT_SHARDS regions handed out in chunks (pt_work.h)
-    const unsigned int units = (unsigned int)P0->til.unit_count;
+    // (pixel, pass) units in PT_SHARDS regions handed out by per-XCD head words (pt_work.h)
+    const unsigned int units = (unsigned int)P0->til.unit_count << batch_log2;
     const EvenRegions regions{units, (units + PT_SHARDS - 1) / PT_SHARDS};
     WorkCursor cursor = work_begin();
     bool drained = false;
@@ -64,8 +71,11 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
             if (want) {
                 if (u != ~0u) {
                     need = false;
-                    pixel = unit_to_pixel(til, u);
+                    unit = u;
+                    const int pixel = unit_to_pixel(til, u >> batch_log2);
+                    const int32_t hseed = hash_pt(first_pass + (int)(u & ((1u << batch_log2) - 1u)));
                     generate_path(P->cam, cfg, pixel, hseed, &ps);
+                    pseed = path_seed(hseed, pixel);
                     depth = 0;
                 } else if (drained) {
                     done = true;
@@ -73,10 +83,10 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
             }
         }
         if (!__any(!done)) break;
-        if (!done && !need) {  // a lane still waiting for a pixel (chunk ran short) has no path yet
+        if (!done && !need) {  // a lane still waiting for a unit (chunk ran short) has no path yet
             bool alive = false;
             if (depth < cfg.max_depth) {
-                alive = trace_step<LEAF1, STATS, PREFETCH>(sc, cfg, pixel, depth, hseed, &ps, &ctr);
+                alive = trace_step<LEAF1, STATS, PREFETCH>(sc, cfg, depth, pseed, &ps, &ctr);
                 depth++;
                 segments++;
                 if (STATS) {
@@ -86,14 +96,20 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
                 }
             }
             if (!alive || depth >= cfg.max_depth) {
-                // pixel_256_transform_gamma_corrected_kernel (:644-680) for this pixel
-                float* img = out.image + (size_t)pixel * 3;
-                v3 c = clamp3(ps.rad, 0.0f, clamp_hi);
-                v3 sum;
-                if (pass != 1) sum = mk3(img[0], img[1], img[2]) + c;
-                else sum = c;
-                img[0] = sum.x; img[1] = sum.y; img[2] = sum.z;
-                if (write_u8 && out.image256) store_u8(cfg, sum, pass, out.image256 + (size_t)pixel * 3);
+                // pixel_256_transform_gamma_corrected_kernel (:644-680) for this (pixel, pass)
+                const v3 c = clamp3(ps.rad, 0.0f, clamp_hi);
+                if (batch_log2 == 0) {
+                    const int pixel = unit_to_pixel(til, unit);
+                    float* img = out.image + (size_t)pixel * 3;
+                    v3 sum;
+                    if (first_pass != 1) sum = mk3(img[0], img[1], img[2]) + c;
+                    else sum = c;
+                    img[0] = sum.x; img[1] = sum.y; img[2] = sum.z;
+                    if (write_u8 && out.image256) store_u8(cfg, sum, first_pass, out.image256 + (size_t)pixel * 3);
+                } else {
+                    float* pr = out.pass_rad + (size_t)unit * 3;
+                    pr[0] = c.x; pr[1] = c.y; pr[2] = c.z;
+                }
                 need = true;
             }
         }
@@ -114,6 +130,26 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
             for (int k = 0; k < 6; k++) atomicAdd(&out0.stats[1 + k], csum[k]);
         }
     }
+}
+
+// The running sum over a batch of passes, in pass order (path_tracer_kernel.cu:644-651 applied
+// pass after pass), then the 8-bit output of the batch's last pass.
+__global__ __launch_bounds__(PT_BLOCK) void accumulate_kernel(const LaunchParams* __restrict__ P, int first_pass,
+                                                              int batch_log2, int write_u8) {
+    const unsigned int lu = blockIdx.x * PT_BLOCK + threadIdx.x;
+    if (lu >= (unsigned int)P->til.unit_count) return;
+    const int pixel = unit_to_pixel(P->til, lu);
+    const int batch = 1 << batch_log2;
+    float* img = P->out.image + (size_t)pixel * 3;
+    const float* pr = P->out.pass_rad + ((size_t)lu << batch_log2) * 3;
+    v3 sum = mk3(img[0], img[1], img[2]);
+    for (int j = 0; j < batch; j++) {
+        const v3 c = mk3(pr[3 * j], pr[3 * j + 1], pr[3 * j + 2]);
+        sum = (first_pass + j == 1) ? c : sum + c;
+    }
+    img[0] = sum.x; img[1] = sum.y; img[2] = sum.z;
+    if (write_u8 && P->out.image256)
+        store_u8(P->cfg, sum, first_pass + batch - 1, P->out.image256 + (size_t)pixel * 3);
 }
 
 // Gamma/8-bit from a float running sum (used after a multi-GPU reduce, and by the reference
@@ -214,7 +250,7 @@ int env_int(const char* name, int dflt, int lo, int hi) {
     return v < lo ? lo : (v > hi ? hi : v);
 }
 
-using PassFn = void (*)(const LaunchParams*, int, int, int);
+using PassFn = void (*)(const LaunchParams*, int, int, int, int);
 
 static bool pass_prefetch() {
     static int p = [] {
@@ -250,14 +286,23 @@ int pass_min_waves() {
     return w;
 }
 
-hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, int pass, int write_u8, int grid, bool stats,
-                       hipStream_t stream) {
+hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, int first_pass, int batch_log2, int write_u8,
+                       int grid, bool stats, hipStream_t stream) {
     PassFn fn = pass_fn(leaf1, stats, pass_min_waves());
     const LaunchParams* a0 = params_dev;
-    int a1 = pass, a2 = write_u8, a3 = env_int("PT_CHUNK_MEGA", 0, 0, 4096);
-    void* args[] = {&a0, &a1, &a2, &a3};
+    static const int chunk = env_int("PT_CHUNK_MEGA", 0, 0, 4096);
+    int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2;
+    void* args[] = {&a0, &a1, &a2, &a3, &a4};
     hipError_t e = hipLaunchKernel((const void*)fn, dim3(grid), dim3(PT_BLOCK), args, 0, stream);
     if (e != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+hipError_t launch_accumulate(const LaunchParams* params_dev, int units, int first_pass, int batch_log2, int write_u8,
+                             hipStream_t stream) {
+    if (units <= 0) return hipSuccess;
+    hipLaunchKernelGGL(accumulate_kernel, dim3((units + PT_BLOCK - 1) / PT_BLOCK), dim3(PT_BLOCK), 0, stream,
+                       params_dev, first_pass, batch_log2, write_u8);
     return hipGetLastError();
 }
 

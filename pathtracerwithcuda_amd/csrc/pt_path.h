@@ -427,27 +427,31 @@ __device__ __forceinline__ Hit closest_hit(const DevScene& sc, v3 o, v3 d, Count
     return h;
 }
 
+// The per-path part of the trace seed hash(seed) * hash(pixel) * hash(depth) (:415), int wrap.
+__device__ __forceinline__ int32_t path_seed(int32_t hseed, int pixel) { return mul_wrap(hseed, hash_pt(pixel)); }
+
 template <bool STATS>
-__device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int pixel, int depth,
-                                          int32_t hseed, PathState* ps, const Hit& h, Counters* ctr);
+__device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
+                                          PathState* ps, const Hit& h, Counters* ctr);
 
 // One invocation of trace_ray_kernel for one live ray (path_tracer_kernel.cu:381-625).
-// Returns false when the reference would write -1 into energy_exist_pixels.
+// pseed = path_seed(hash(pass), pixel). Returns false when the reference would write -1 into
+// energy_exist_pixels.
 template <bool LEAF1, bool STATS, bool PREFETCH>
-__device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& cfg, int pixel, int depth,
-                                           int32_t hseed, PathState* ps, Counters* ctr) {
+__device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
+                                           PathState* ps, Counters* ctr) {
     const Hit h = closest_hit<LEAF1, STATS, PREFETCH>(sc, ps->o, ps->d, ctr);
-    return shade_hit<STATS>(sc, cfg, pixel, depth, hseed, ps, h, ctr);
+    return shade_hit<STATS>(sc, cfg, depth, pseed, ps, h, ctr);
 }
 
 // The part of trace_ray_kernel after the closest hit is known (:456-624): medium, material,
 // Fresnel-selected bounce, accumulation, kill test.
 template <bool STATS>
-__device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int pixel, int depth,
-                                          int32_t hseed, PathState* ps, const Hit& h, Counters* ctr) {
+__device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
+                                          PathState* ps, const Hit& h, Counters* ctr) {
     const v3 o = ps->o, d = ps->d;
     const float min_t = h.t;
-    minstd rng = minstd_seed(mul_wrap(mul_wrap(hseed, hash_pt(pixel)), hash_pt(depth)));
+    minstd rng = minstd_seed(mul_wrap(pseed, hash_pt(depth)));
 
     // medium: absorption and subsurface scattering (:456-492)
     {

@@ -245,6 +245,9 @@ struct pt_context {
     void* wave_mem = nullptr;
     size_t wave_bytes = 0;
     DevWave wave{};
+    // batched passes of the single-kernel schedule: clamped radiance per (unit, pass)
+    float* pass_rad = nullptr;
+    size_t pass_rad_bytes = 0;
     // thread_shrink scratch
     int* shrink_buf = nullptr;
     int* shrink_tiles = nullptr;
@@ -413,6 +416,7 @@ int ensure_wave(pt_context* ctx, int units, int depth) {
     for (int i = 0; i < 8; i++) { off[i] = total; total = (total + sizes[i] + 255) & ~(size_t)255; }
     if (total > ctx->wave_bytes) {
         if (ctx->wave_mem) (void)hipFree(ctx->wave_mem);
+    if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
         ctx->wave_mem = nullptr;
         ctx->wave_bytes = 0;
         PT_HIP(hipMalloc(&ctx->wave_mem, total));
@@ -431,6 +435,18 @@ int ensure_wave(pt_context* ctx, int units, int depth) {
     w.heads = w.counters + ((size_t)PT_SHARDS * (depth + 1) * sizeof(unsigned int) + 255) / 256 * 64;
     w.seg_cap = seg_cap;
     return PT_OK;
+}
+
+// Passes per single-kernel launch (power of two); PT_PASS_BATCH overrides (1 = one launch per pass).
+int max_pass_batch() {
+    static int b = [] {
+        const char* e = getenv("PT_PASS_BATCH");
+        int v = e ? atoi(e) : 8;
+        int p = 1;
+        while (p * 2 <= v && p < 64) p *= 2;
+        return p;
+    }();
+    return b;
 }
 
 // PT_MODE=wave selects the extend/shade wavefront schedule; the default is the single persistent
@@ -452,7 +468,7 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     DevConfig dc = to_dev(*config);
     DevCamera dcam = to_dev(*cam);
     update_tiling(ctx);
-    DevOutput out;
+    DevOutput out{};
     out.image = ctx->image;
     out.image256 = ctx->image256;
     out.fetch = ctx->fetch;
@@ -489,16 +505,41 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         }
         return PT_OK;
     }
+    // Single-kernel schedule: up to max_pass_batch() passes per launch (pt_kernels.hip pass_kernel),
+    // a power of two so a unit splits into (pixel, pass) by shift and mask.
     const int grid = pass_grid(ctx);
+    const int units = ctx->tiling.unit_count;
+    int most = 1;
+    while (most * 2 <= max_pass_batch() && (long long)units * most * 2 <= (1ll << 28)) most *= 2;
+    if (most > 1 && pass_count > 1) {
+        const size_t need = (size_t)units * (size_t)most * 12;
+        if (need > ctx->pass_rad_bytes) {
+            if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
+            ctx->pass_rad = nullptr;
+            ctx->pass_rad_bytes = 0;
+            PT_HIP(hipMalloc(&ctx->pass_rad, need));
+            ctx->pass_rad_bytes = need;
+        }
+    }
+    lp.out.pass_rad = ctx->pass_rad;
     PT_HIP(hipMemcpyAsync(ctx->params, &lp, sizeof(lp), hipMemcpyHostToDevice, ctx->stream));
-    for (int i = 0; i < pass_count; i++) {
-        int pass = first_pass + i;
-        int w8 = write_u8 == 1 || (write_u8 == 2 && i == pass_count - 1);
+    for (int i = 0; i < pass_count;) {
+        int b = 1, lg = 0;
+        while (b * 2 <= most && i + b * 2 <= pass_count) { b *= 2; lg++; }
+        const int first = first_pass + i;
+        const int last = i + b == pass_count;
+        const int w8 = write_u8 == 1 || (write_u8 == 2 && last);
         PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
         int rc = ev_begin(ctx, 0);
         if (rc != PT_OK) return rc;
-        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, pass, w8, grid, ctx->instrumented, ctx->stream));
+        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, first, lg, w8, grid, ctx->instrumented, ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
+        if (lg > 0) {
+            if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;
+            PT_HIP(launch_accumulate(ctx->params, units, first, lg, w8, ctx->stream));
+            if ((rc = ev_end(ctx)) != PT_OK) return rc;
+        }
+        i += b;
     }
     return PT_OK;
 }

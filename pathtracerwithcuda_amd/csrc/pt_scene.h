@@ -113,6 +113,7 @@ struct DevOutput {
     uint8_t* image256;       // uchar3 (3 B stride), may be null
     unsigned int* fetch;     // PT_HEAD_SET work heads of the single-kernel pass (zeroed before launch)
     unsigned long long* stats;  // [0] ray segments, [1..] optional instrumentation
+    float* pass_rad;         // batched passes: clamped radiance per (unit, pass) (12 B), summed in order
 };
 
 // Wavefront queues (pt_wavefront.hip). Ray slots are dense per depth; path state is per pixel.

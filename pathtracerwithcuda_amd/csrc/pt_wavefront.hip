@@ -218,7 +218,7 @@ __global__ __launch_bounds__(PT_BLOCK) void shade_kernel(const LaunchParams* __r
                 const int code = __float_as_int(hh.w);
                 h.type = code & 3;
                 h.prim = code >> 2;
-                alive = shade_hit<STATS>(sc, cfg, pixel, depth, hseed, &ps, h, &ctr);
+                alive = shade_hit<STATS>(sc, cfg, depth, path_seed(hseed, pixel), &ps, h, &ctr);
                 W.st_rad[pixel] = make_float4(ps.rad.x, ps.rad.y, ps.rad.z, 0.0f);
                 if (!LAST && alive)
                     W.st_thr[pixel] = make_float4(ps.thr.x, ps.thr.y, ps.thr.z, __int_as_float(ps.medium));
