@@ -19,6 +19,20 @@
 
 namespace pt {
 
+// A copy of *p read through the constant address space: the loads are known not to alias the
+// kernel's stores, so a wave-uniform p becomes scalar loads into SGPRs (s_load_dwordx*), not
+// vector loads that cost VGPRs and vector-memory issue slots.
+template <class T>
+__device__ __forceinline__ T load_const(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(4))) const T ConstT;
+    const ConstT* c = (const ConstT*)(unsigned long long)p;
+    return *c;
+#else
+    return *p;
+#endif
+}
+
 // MINW = minimum waves per SIMD requested from the register allocator; the persistent loop is
 // latency-bound, so occupancy is the first-order knob.
 //
@@ -28,13 +42,10 @@ namespace pt {
 // With B == 1 a finished path accumulates into the image directly; with B > 1 it stores its clamped
 // radiance in pass_rad[u] and accumulate_kernel sums the passes in pass order afterwards, so the
 // running sum is bit-identical to one launch per pass.
-template <bool LEAF1, bool STATS, int MINW, bool PREFETCH>
+template <bool LEAF1, bool STATS, int MINW, bool QN>
 __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams* __restrict__ params, int first_pass,
                                                               int write_u8, int chunk, int batch_log2) {
     const int lane = threadIdx.x & 63;
-    // The launch parameters live in device memory and are re-read (scalar loads, K$ hits) inside
-    // every iteration instead of being pinned in SGPRs for the whole kernel: the empty asm makes
-    // the pointer opaque per iteration so loop-invariant code motion cannot hoist the fields.
     const LaunchParams* P0 = params;
     const DevConfig& cfg0 = P0->cfg;
     const DevOutput& out0 = P0->out;
@@ -57,12 +68,17 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
     bool drained = false;
 
     while (true) {
+        // The launch parameters are re-read every iteration (scalar loads, K$ hits) rather than held
+        // in registers across the whole loop: the empty asm hides the pointer from loop-invariant
+        // code motion; readfirstlane restores its uniformity (asm results count as divergent), and
+        // the constant-address-space read makes the loads scalar (s_load into SGPRs).
         const LaunchParams* P = params;
         asm volatile("" : "+s"(P));
-        const DevScene& sc = P->sc;
-        const DevConfig& cfg = P->cfg;
-        const DevTiling& til = P->til;
-        const DevOutput& out = P->out;
+        P = uniform_ptr(P);
+        const DevScene sc = load_const(&P->sc);
+        const DevConfig cfg = load_const(&P->cfg);
+        const DevTiling til = load_const(&P->til);
+        const DevOutput out = load_const(&P->out);
         const bool want = need && !done;
         const unsigned long long need_mask = __ballot(want);
         if (need_mask) {
@@ -74,7 +90,8 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
                     unit = u;
                     const int pixel = unit_to_pixel(til, u >> batch_log2);
                     const int32_t hseed = hash_pt(first_pass + (int)(u & ((1u << batch_log2) - 1u)));
-                    generate_path(P->cam, cfg, pixel, hseed, &ps);
+                    const DevCamera cam = load_const(&P->cam);
+                    generate_path(cam, cfg, pixel, hseed, &ps);
                     pseed = path_seed(hseed, pixel);
                     depth = 0;
                 } else if (drained) {
@@ -86,7 +103,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
         if (!done && !need) {  // a lane still waiting for a unit (chunk ran short) has no path yet
             bool alive = false;
             if (depth < cfg.max_depth) {
-                alive = trace_step<LEAF1, STATS, PREFETCH>(sc, cfg, depth, pseed, &ps, &ctr);
+                alive = trace_step<LEAF1, STATS, QN>(sc, cfg, depth, pseed, &ps, &ctr);
                 depth++;
                 segments++;
                 if (STATS) {
@@ -252,43 +269,39 @@ int env_int(const char* name, int dflt, int lo, int hi) {
 
 using PassFn = void (*)(const LaunchParams*, int, int, int, int);
 
-static bool pass_prefetch() {
-    static int p = [] {
-        const char* e = getenv("PT_PREFETCH");
-        return e ? atoi(e) : 0;
-    }();
-    return p != 0;
-}
-
-static PassFn pass_fn(bool leaf1, bool stats, int minw) {
-    const bool pf = pass_prefetch();
+// QN (quantised nodes) only for leaf size 1 and the uninstrumented kernel: the instrumented kernel
+// walks the exact nodes so its visit counts are the reference's.
+static PassFn pass_fn(bool leaf1, bool stats, int minw, bool qn) {
     if (leaf1 && !stats) {
-        if (pf) {
-            if (minw == 4) return pass_kernel<true, false, 4, true>;
+        if (qn) {
             if (minw == 6) return pass_kernel<true, false, 6, true>;
+            if (minw == 7) return pass_kernel<true, false, 7, true>;
+            if (minw == 8) return pass_kernel<true, false, 8, true>;
             return pass_kernel<true, false, 5, true>;
         }
         if (minw == 4) return pass_kernel<true, false, 4, false>;
         if (minw == 6) return pass_kernel<true, false, 6, false>;
+        if (minw == 7) return pass_kernel<true, false, 7, false>;
+        if (minw == 8) return pass_kernel<true, false, 8, false>;
         return pass_kernel<true, false, 5, false>;
     }
-    if (leaf1 && stats) return pass_kernel<true, true, 5, true>;
-    if (!stats) return pass_kernel<false, false, 5, true>;
-    return pass_kernel<false, true, 5, true>;
+    if (leaf1 && stats) return pass_kernel<true, true, 5, false>;
+    if (!stats) return pass_kernel<false, false, 5, false>;
+    return pass_kernel<false, true, 5, false>;
 }
 
 int pass_min_waves() {
     static int w = [] {
         const char* e = getenv("PT_MIN_WAVES");
-        int v = e ? atoi(e) : 6;
-        return (v == 4 || v == 5 || v == 6) ? v : 6;
+        int v = e ? atoi(e) : 8;
+        return (v >= 4 && v <= 8) ? v : 8;
     }();
     return w;
 }
 
-hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, int first_pass, int batch_log2, int write_u8,
-                       int grid, bool stats, hipStream_t stream) {
-    PassFn fn = pass_fn(leaf1, stats, pass_min_waves());
+hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int first_pass, int batch_log2,
+                       int write_u8, int grid, bool stats, hipStream_t stream) {
+    PassFn fn = pass_fn(leaf1, stats, pass_min_waves(), qn);
     const LaunchParams* a0 = params_dev;
     static const int chunk = env_int("PT_CHUNK_MEGA", 0, 0, 4096);
     int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2;
@@ -314,11 +327,11 @@ hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256
     return hipGetLastError();
 }
 
-int pass_grid_size(bool leaf1, bool stats) {
+int pass_grid_size(bool leaf1, bool stats, bool qn) {
     int dev = 0, cus = 0, blocks = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* fn = (const void*)pass_fn(leaf1, stats, pass_min_waves());
+    const void* fn = (const void*)pass_fn(leaf1, stats, pass_min_waves(), qn);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, PT_BLOCK, 0) != hipSuccess || blocks <= 0) blocks = 4;
     if (cus <= 0) cus = 256;
     return cus * blocks;

@@ -30,8 +30,21 @@ __device__ __forceinline__ int f2i(float f) { return __float_as_int(f); }
 // Scene records through buffer descriptors: a raw_buffer_load_b128 is never narrowed by the
 // compiler and is only waited for at its first use, so a load can be issued early (prefetch).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// Wave-uniform copies of scene pointers and sizes. Inside the divergent path loop the compiler can
+// lose track of their uniformity and keep them in VGPRs; a buffer descriptor held in VGPRs turns
+// every buffer load into a waterfall loop (readfirstlane x4, compare, exec juggling per load). The
+// scene is the same for every lane, so readfirstlane is exact and pins them to SGPRs.
+__device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned int lo = (unsigned int)__builtin_amdgcn_readfirstlane((int)(unsigned int)v);
+    const unsigned int hi = (unsigned int)__builtin_amdgcn_readfirstlane((int)(unsigned int)(v >> 32));
+    return (T*)(((unsigned long long)hi << 32) | lo);
+}
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_ptr(base)), (short)0, uniform_int(bytes),
+                                             0x00020000);
 }
 __device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int byte_offset) {
     u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_offset, 0, 0);
@@ -269,11 +282,9 @@ struct Counters {
     unsigned int scatter;     // subsurface free-flight event (no surface shading)
 };
 
-// path_tracer_kernel.cu:85-161: stackless preorder walk with skip indices over one mesh.
-// PREFETCH: in preorder the node after a hit (or a leaf) is always pos+1, so its record is requested
-// while node pos is tested; a miss jumps to next_node_index and pays the full latency. The node
-// sequence, the tests and therefore the result are exactly the reference's.
-template <bool LEAF1, bool STATS, bool PREFETCH>
+// path_tracer_kernel.cu:85-161: stackless preorder walk with skip indices over one mesh, on the
+// exact 32-B node records (the reference's own node sequence: the STATS kernels count its visits).
+template <bool LEAF1, bool STATS>
 __device__ __forceinline__ bool mesh_closest(const DevScene& sc, int begin, int end, v3 o, v3 d, v3 inv,
                                              float* ht, float* ht1, float* ht2, int* htri, Counters* ctr) {
     const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
@@ -283,20 +294,12 @@ __device__ __forceinline__ bool mesh_closest(const DevScene& sc, int begin, int 
     int min_tri = -1;
     bool hit = false;
     int pos = begin;
-    if (pos == end) return false;
-    float4 lo = bload(rn, pos * 32), hi = bload(rn, pos * 32 + 16);
-    float4 nlo, nhi;
-    if (PREFETCH) { nlo = bload(rn, pos * 32 + 32); nhi = bload(rn, pos * 32 + 48); }
-    while (true) {
+    while (pos != end) {
+        const float4 lo = bload(rn, pos * 32), hi = bload(rn, pos * 32 + 16);
         if (STATS) ctr->nodes++;
         float entry;
         if (box_hit(lo, hi, o, inv, &entry) && entry <= min_t) {
             const int slot = f2i(hi.w);
-            pos++;
-            if (PREFETCH) {
-                lo = nlo; hi = nhi;
-                if (pos != end) { nlo = bload(rn, pos * 32 + 32); nhi = bload(rn, pos * 32 + 48); }
-            }
             if (slot >= 0) {
                 if (LEAF1) {
                     float t, t1, t2;
@@ -318,13 +321,61 @@ __device__ __forceinline__ bool mesh_closest(const DevScene& sc, int begin, int 
                     }
                 }
             }
-            if (pos == end) break;
-            if (!PREFETCH) { lo = bload(rn, pos * 32); hi = bload(rn, pos * 32 + 16); }
+            pos++;
         } else {
             pos = f2i(lo.w);
-            if (pos == end) break;
-            lo = bload(rn, pos * 32); hi = bload(rn, pos * 32 + 16);
-            if (PREFETCH) { nlo = bload(rn, pos * 32 + 32); nhi = bload(rn, pos * 32 + 48); }
+        }
+    }
+    if (hit) { *ht = min_t; *ht1 = min_t1; *ht2 = min_t2; *htri = min_tri; }
+    return hit;
+}
+
+// The same walk on 16-B quantised nodes (leaf size 1; DESIGN.md §3.1 "quantised nodes"). Each node
+// box is rounded OUTWARD to 16-bit fixed point in its mesh's frame, so it contains the exact box and
+// the walk visits every node the reference visits (plus a few more). A leaf (link < 0) holds its
+// triangle; its skip index is pos + 1. A triangle hit only counts if the reference's own leaf test
+// passes with the exact leaf box and the current min_t — the test every ancestor's exact test
+// implies (box containment, monotone rounding) — so the result is exactly the reference's: the
+// same hits, accepted in the same preorder, under the same min_t. One 16-B load per node instead of
+// two halves the vector-memory instructions, which bound this loop (TA/TD busy).
+__device__ __forceinline__ bool mesh_closest_q(const DevScene& sc, int mesh, int begin, int end, v3 o, v3 d, v3 inv,
+                                               float* ht, float* ht1, float* ht2, int* htri) {
+    const __amdgpu_buffer_rsrc_t rq = make_rsrc(sc.qnodes, sc.node_count * 16);
+    const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
+    const __amdgpu_buffer_rsrc_t rt = make_rsrc(sc.tri_geom, sc.tri_count * 48);
+    const float4* mq = uniform_ptr(sc.mesh_q);
+    const float4 fb = mq[2 * mesh], fs = mq[2 * mesh + 1];
+    float min_t = __builtin_inff();
+    float min_t1 = 0.0f, min_t2 = 0.0f;
+    int min_tri = -1;
+    bool hit = false;
+    int pos = begin;
+    while (pos != end) {
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rq, pos * 16, 0, 0);
+        float4 lo, hi;
+        lo.x = fb.x + (float)(q.x & 0xffffu) * fs.x;
+        lo.y = fb.y + (float)(q.x >> 16) * fs.y;
+        lo.z = fb.z + (float)(q.y & 0xffffu) * fs.z;
+        hi.x = fb.x + (float)(q.y >> 16) * fs.x;
+        hi.y = fb.y + (float)(q.z & 0xffffu) * fs.y;
+        hi.z = fb.z + (float)(q.z >> 16) * fs.z;
+        const int link = (int)q.w;
+        float entry;
+        if (box_hit(lo, hi, o, inv, &entry) && entry <= min_t) {
+            if (link < 0) {
+                const int tri = link & 0x7fffffff;
+                float t, t1, t2;
+                float4 a = bload(rt, tri * 48), b = bload(rt, tri * 48 + 16), c = bload(rt, tri * 48 + 32);
+                if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < min_t) {
+                    float ee;
+                    if (box_hit(bload(rn, pos * 32), bload(rn, pos * 32 + 16), o, inv, &ee) && ee <= min_t) {
+                        min_t = t; min_t1 = t1; min_t2 = t2; min_tri = tri; hit = true;
+                    }
+                }
+            }
+            pos++;
+        } else {
+            pos = link < 0 ? pos + 1 : link;
         }
     }
     if (hit) { *ht = min_t; *ht1 = min_t1; *ht2 = min_t2; *htri = min_tri; }
@@ -402,7 +453,8 @@ struct Hit {
     int prim;
 };
 
-template <bool LEAF1, bool STATS, bool PREFETCH>
+// QN: walk the quantised nodes (LEAF1 && !STATS && sc.qnodes, chosen on the host).
+template <bool LEAF1, bool STATS, bool QN>
 __device__ __forceinline__ Hit closest_hit(const DevScene& sc, v3 o, v3 d, Counters* ctr) {
     Hit h;
     h.t = __builtin_inff(); h.t1 = __builtin_inff(); h.t2 = __builtin_inff();
@@ -416,10 +468,12 @@ __device__ __forceinline__ Hit closest_hit(const DevScene& sc, v3 o, v3 d, Count
     if (sc.mesh_num > 0) {
         v3 inv = 1.0f / d;
         for (int m = 0; m < sc.mesh_num; m++) {
-            int2 r = sc.mesh_range[m];
+            const int2 r = uniform_ptr(sc.mesh_range)[m];
             float t, t1, t2;
             int tri;
-            if (mesh_closest<LEAF1, STATS, PREFETCH>(sc, r.x, r.y, o, d, inv, &t, &t1, &t2, &tri, ctr) && t < h.t && t > 0.0f) {
+            const bool mh = QN ? mesh_closest_q(sc, m, r.x, r.y, o, d, inv, &t, &t1, &t2, &tri)
+                               : mesh_closest<LEAF1, STATS>(sc, r.x, r.y, o, d, inv, &t, &t1, &t2, &tri, ctr);
+            if (mh && t < h.t && t > 0.0f) {
                 h.t = t; h.t1 = t1; h.t2 = t2; h.prim = tri; h.type = 2;
             }
         }
@@ -437,10 +491,10 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
 // One invocation of trace_ray_kernel for one live ray (path_tracer_kernel.cu:381-625).
 // pseed = path_seed(hash(pass), pixel). Returns false when the reference would write -1 into
 // energy_exist_pixels.
-template <bool LEAF1, bool STATS, bool PREFETCH>
+template <bool LEAF1, bool STATS, bool QN>
 __device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
                                            PathState* ps, Counters* ctr) {
-    const Hit h = closest_hit<LEAF1, STATS, PREFETCH>(sc, ps->o, ps->d, ctr);
+    const Hit h = closest_hit<LEAF1, STATS, QN>(sc, ps->o, ps->d, ctr);
     return shade_hit<STATS>(sc, cfg, depth, pseed, ps, h, ctr);
 }
 

@@ -7,9 +7,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -46,9 +48,12 @@ void set_error(const char* fmt, ...) {
 
 inline float4 mkf4(float x, float y, float z, float w) { float4 r; r.x = x; r.y = y; r.z = z; r.w = w; return r; }
 inline float i2f(int i) { float f; std::memcpy(&f, &i, 4); return f; }
+inline int f2i_host(float f) { int i; std::memcpy(&i, &f, 4); return i; }
 
 struct SceneStage {
     std::vector<float4> nodes;
+    std::vector<uint4> qnodes;     // empty: quantised walk unavailable (leaf size > 1, odd input)
+    std::vector<float4> mesh_q;
     std::vector<int> leaf_tris;
     std::vector<int2> mesh_range;
     std::vector<float4> tri_geom, tri_shade, spheres;
@@ -78,6 +83,86 @@ DevMaterial to_dev(const pt_material& m) {
     d.diffuse_texture_id = m.diffuse_texture_id;
     d.specular_texture_id = m.specular_texture_id;
     return d;
+}
+
+// 16-bit fixed-point node boxes (pt_scene.h qnodes, pt_path.h mesh_closest_q). The dequantised
+// plane is origin + (float)q * step, evaluated by the device with the same two IEEE operations (no
+// contraction); q is chosen so that the plane lies outside (or on) the exact one, which is all the
+// walk needs for exactness.
+float dequant(float origin, float step, unsigned q) { return origin + (float)q * step; }
+
+unsigned quant_down(float origin, float step, float v) {
+    if (!(step > 0.0f)) return 0;
+    double f = std::floor(((double)v - (double)origin) / (double)step);
+    long long q = f < 0 ? 0 : (f > 65535 ? 65535 : (long long)f);
+    while (q > 0 && dequant(origin, step, (unsigned)q) > v) q--;
+    while (q < 65535 && dequant(origin, step, (unsigned)q + 1) <= v) q++;
+    return (unsigned)q;
+}
+
+unsigned quant_up(float origin, float step, float v) {
+    if (!(step > 0.0f)) return 0;
+    double f = std::ceil(((double)v - (double)origin) / (double)step);
+    long long q = f < 0 ? 0 : (f > 65535 ? 65535 : (long long)f);
+    while (q < 65535 && dequant(origin, step, (unsigned)q) < v) q++;
+    while (q > 0 && dequant(origin, step, (unsigned)q - 1) >= v) q--;
+    return (unsigned)q;
+}
+
+// Builds st.qnodes / st.mesh_q from st.nodes (leaf size 1). Leaves the vectors empty if a node is
+// not representable (non-finite box, a leaf whose skip index is not pos + 1, a box outside the
+// frame); the pass kernel then walks the exact nodes.
+void quantise_nodes(SceneStage& st) {
+    st.qnodes.clear();
+    st.mesh_q.clear();
+    if (st.leaf_size != 1) return;
+    std::vector<uint4> q(st.nodes.size() / 2);
+    for (const int2& r : st.mesh_range) {
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = r.x; i < r.y; i++) {
+            const float4& a = st.nodes[2 * i];
+            const float4& b = st.nodes[2 * i + 1];
+            const float l[3] = {a.x, a.y, a.z}, h[3] = {b.x, b.y, b.z};
+            for (int k = 0; k < 3; k++) {
+                if (!std::isfinite(l[k]) || !std::isfinite(h[k])) return;
+                lo[k] = std::min(lo[k], l[k]);
+                hi[k] = std::max(hi[k], h[k]);
+            }
+        }
+        float step[3] = {0.0f, 0.0f, 0.0f};
+        for (int k = 0; k < 3; k++) {
+            if (r.x == r.y || hi[k] <= lo[k]) continue;
+            step[k] = (float)(((double)hi[k] - (double)lo[k]) / 65534.0);
+            if (!(step[k] > 0.0f)) step[k] = std::numeric_limits<float>::denorm_min();
+            while (dequant(lo[k], step[k], 65535u) < hi[k]) step[k] = std::nextafter(step[k], INFINITY);
+        }
+        st.mesh_q.push_back(mkf4(lo[0], lo[1], lo[2], 0.0f));
+        st.mesh_q.push_back(mkf4(step[0], step[1], step[2], 0.0f));
+        for (int i = r.x; i < r.y; i++) {
+            const float4& a = st.nodes[2 * i];
+            const float4& b = st.nodes[2 * i + 1];
+            const float l[3] = {a.x, a.y, a.z}, h[3] = {b.x, b.y, b.z};
+            unsigned ql[3], qh[3];
+            for (int k = 0; k < 3; k++) {
+                ql[k] = quant_down(lo[k], step[k], l[k]);
+                qh[k] = quant_up(lo[k], step[k], h[k]);
+                if (dequant(lo[k], step[k], ql[k]) > l[k] || dequant(lo[k], step[k], qh[k]) < h[k]) return;
+            }
+            const int next = f2i_host(a.w), slot = f2i_host(b.w);
+            uint4 n;
+            n.x = ql[0] | (ql[1] << 16);
+            n.y = ql[2] | (qh[0] << 16);
+            n.z = qh[1] | (qh[2] << 16);
+            if (slot >= 0) {
+                if (next != i + 1) return;
+                n.w = 0x80000000u | (unsigned)slot;
+            } else {
+                n.w = (unsigned)next;
+            }
+            q[i] = n;
+        }
+    }
+    st.qnodes.swap(q);
 }
 
 // Reference layout -> device layout (pt_scene.h). Reads every embedded pointer on the host.
@@ -120,6 +205,7 @@ int translate_scene(SceneStage& st, int mesh_num, pt_bvh_node_device** bvh_nodes
     }
     const int T = tri_num >= 0 ? tri_num : max_tri + 1;
     if (max_tri >= T) { set_error("bvh references triangle %d >= triangle_num %d", max_tri, T); return PT_E_ARG; }
+    quantise_nodes(st);
 
     std::unordered_map<const pt_material*, int> mat_index;
     int max_tex = -1;
@@ -237,7 +323,7 @@ struct pt_context {
     LaunchParams* params = nullptr;  // device copy of the launch parameter block
     bool instrumented = false;
     int schedule = -1;  // PT_SCHEDULE_*; -1: environment default (PT_MODE)
-    int grid[2][2] = {{0, 0}, {0, 0}};
+    int grid[2][2][2] = {};
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
     size_t ev_used = 0;
@@ -295,6 +381,8 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     size_t i_tex = add(st.tex_desc.data(), st.tex_desc.size() * sizeof(int4));
     size_t i_pool = add(st.tex_pool.data(), st.tex_pool.size());
     size_t i_cube = add(st.cube.data(), st.cube.size());
+    size_t i_q = add(st.qnodes.data(), st.qnodes.size() * sizeof(uint4));
+    size_t i_mq = add(st.mesh_q.data(), st.mesh_q.size() * sizeof(float4));
     free_scene(ctx);
     if (total == 0) total = 256;
     PT_HIP(hipMalloc(&ctx->scene_mem, total));
@@ -314,6 +402,8 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     s.tex_desc = (const int4*)(base + pieces[i_tex].off);
     s.tex_pool = (const uint8_t*)(base + pieces[i_pool].off);
     s.cube = (const uint8_t*)(base + pieces[i_cube].off);
+    s.qnodes = st.qnodes.empty() ? nullptr : (const uint4*)(base + pieces[i_q].off);
+    s.mesh_q = st.mesh_q.empty() ? nullptr : (const float4*)(base + pieces[i_mq].off);
     s.mesh_num = (int)st.mesh_range.size();
     s.sphere_num = (int)(st.spheres.size() / 2);
     s.leaf_size = st.leaf_size;
@@ -369,10 +459,20 @@ void update_tiling(pt_context* ctx) {
     t.unit_count = rows * ctx->width;
 }
 
+// PT_QNODES=1 walks the 16-B quantised nodes (bit-identical; measured slower than the exact
+// 32-B walk on MI355X at 1080p, DESIGN.md §3.1, so off by default).
+bool use_qnodes(const pt_context* ctx) {
+    static int on = [] {
+        const char* e = getenv("PT_QNODES");
+        return e && atoi(e) != 0;
+    }();
+    return on && ctx->scene.qnodes != nullptr;
+}
+
 int pass_grid(pt_context* ctx) {
-    bool leaf1 = ctx->scene.leaf_size == 1;
-    int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0];
-    if (g == 0) g = pass_grid_size(leaf1, ctx->instrumented);
+    const bool leaf1 = ctx->scene.leaf_size == 1, qn = use_qnodes(ctx);
+    int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0][qn ? 1 : 0];
+    if (g == 0) g = pass_grid_size(leaf1, ctx->instrumented, qn);
     return g;
 }
 
@@ -532,7 +632,8 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
         int rc = ev_begin(ctx, 0);
         if (rc != PT_OK) return rc;
-        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, first, lg, w8, grid, ctx->instrumented, ctx->stream));
+        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, use_qnodes(ctx), first, lg, w8, grid,
+                           ctx->instrumented, ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         if (lg > 0) {
             if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;

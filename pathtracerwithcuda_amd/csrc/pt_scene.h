@@ -18,6 +18,9 @@
 //   materials  DevMaterial[M] (96 B), sphere materials appended after mesh materials
 //   textures   int4[K] {width, height, byte offset, -} + one RGBA8 byte pool
 //   cube       RGBA8, 6 faces back to back (x+, x-, y+, y-, z+, z-), length^2 texels each
+//   qnodes     uint4[N] per node, same preorder index as `nodes`: lo.xyz, hi.xyz as u16 fixed point
+//              (value = origin + q * step in the mesh's frame, rounded outward), then a link word:
+//              internal -> next_node_index, leaf -> 0x80000000 | triangle id            16 B/node
 #pragma once
 
 #include <stdint.h>
@@ -28,6 +31,7 @@
 struct alignas(16) float4 { float x, y, z, w; };
 struct alignas(8) int2 { int x, y; };
 struct alignas(16) int4 { int x, y, z, w; };
+struct alignas(16) uint4 { unsigned int x, y, z, w; };
 #endif
 
 namespace pt {
@@ -59,6 +63,8 @@ struct DevScene {
     const int4* tex_desc;
     const uint8_t* tex_pool;
     const uint8_t* cube;
+    const uint4* qnodes;     // 16-B quantised nodes (leaf size 1), or null: see below
+    const float4* mesh_q;    // per mesh {frame origin}, {frame step} of the quantised nodes
     int mesh_num;
     int sphere_num;
     int leaf_size;
