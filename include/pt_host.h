@@ -31,6 +31,13 @@ extern "C" {
 int pt_bvh_build(const pt_triangle* triangles, int n, int start_index, int leaf_size, int method,
                  pt_bvh_node_device** nodes, int* node_num, int** leaf_indices, int* leaf_num);
 void pt_bvh_free(pt_bvh_node_device* nodes, int* leaf_indices);
+/* Any of the three configured builders (pt_bvh_build_method): NaiveCPU = the bucketed "SAH"
+ * builder (Bvh/bvh.cpp:16-219, bucket_num = BvhBucketMaxDivideInternalNum); MortonCodeCPU and
+ * MortonCodeCUDA = the Morton builder above. Same output contract as pt_bvh_build. */
+int pt_bvh_build_ex(const pt_triangle* triangles, int n, int start_index, int leaf_size, int method, int bucket_num,
+                    pt_bvh_node_device** nodes, int* node_num, int** leaf_indices, int* leaf_num);
+int pt_bvh_build_naive(const pt_triangle* triangles, int n, int start_index, int leaf_size, int bucket_num,
+                       pt_bvh_node_device** nodes, int* node_num, int** leaf_indices, int* leaf_num);
 
 /* Morton helpers exposed for known-answer tests (Bvh/bvh.cpp:370-441). */
 unsigned int pt_morton_code(float x, float y, float z);
@@ -73,6 +80,7 @@ int pt_scene_builder_set_cube_map(pt_scene_builder* b, int length, const unsigne
 int pt_scene_builder_add_texture(pt_scene_builder* b, int width, int height, const unsigned char* rgba);
 /* Builds every mesh BVH and fixes up the embedded pointers. */
 int pt_scene_builder_build(pt_scene_builder* b, int leaf_size, int method);
+int pt_scene_builder_build_ex(pt_scene_builder* b, int leaf_size, int method, int bucket_num);
 int pt_scene_builder_view(pt_scene_builder* b, pt_scene_view* out);
 
 /* ---- camera (Core/camera.cpp) --------------------------------------------------------------- */

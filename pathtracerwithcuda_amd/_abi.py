@@ -142,6 +142,20 @@ class ViewCamera(C.Structure):  # include/pt_host.h (Core/camera.h:27-80)
     ]
 
 
+class ObjMesh(C.Structure):  # include/pt_loader.h
+    _fields_ = [
+        ("triangle_num", C.c_int), ("shape_num", C.c_int), ("vertex_num", C.c_int),
+        ("vertices", c_float_p), ("normals", c_float_p), ("uvs", c_float_p), ("shape_of_triangle", c_int_p),
+    ]
+
+
+class SceneLoadOptions(C.Structure):  # include/pt_loader.h
+    _fields_ = [
+        ("root_dir", C.c_char_p), ("background_override", C.c_char_p), ("background_format", C.c_char_p),
+        ("leaf_size", C.c_int), ("bvh_method", C.c_int), ("bucket_num", C.c_int),
+    ]
+
+
 LAYOUT = {  # include/pt_types.h static asserts
     "Ray": 24, "Scattering": 24, "Medium": 32, "Material": 84, "Sphere": 100, "Triangle": 104,
     "BoundingBox": 36, "BvhNodeDevice": 56, "RenderCamera": 64, "Configuration": 96, "CubeMap": 56,
@@ -206,6 +220,20 @@ _PROTOS = {
     "pt_view_camera_set_fov": (None, [C.POINTER(ViewCamera), C.c_float]),
     "pt_view_camera_get_render_camera": (None, [C.POINTER(ViewCamera), C.POINTER(RenderCamera)]),
     "pt_configuration_default": (None, [C.POINTER(Configuration)]),
+    "pt_bvh_build_ex": (C.c_int, [C.POINTER(Triangle), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.POINTER(C.POINTER(BvhNodeDevice)), c_int_p, C.POINTER(c_int_p), c_int_p]),
+    "pt_bvh_build_naive": (C.c_int, [C.POINTER(Triangle), C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.POINTER(C.POINTER(BvhNodeDevice)), c_int_p, C.POINTER(c_int_p), c_int_p]),
+    "pt_scene_builder_build_ex": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
+    # ingestion (include/pt_loader.h)
+    "pt_config_load": (C.c_int, [C.c_char_p, C.POINTER(Configuration)]),
+    "pt_material_preset": (C.c_int, [C.c_char_p, C.POINTER(Material)]),
+    "pt_obj_load": (C.c_int, [C.c_char_p, C.POINTER(ObjMesh)]),
+    "pt_obj_free": (None, [C.POINTER(ObjMesh)]),
+    "pt_scene_load": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(SceneLoadOptions)]),
+    "pt_image_load": (C.c_int, [C.c_char_p, c_int_p, c_int_p, C.POINTER(c_ubyte_p)]),
+    "pt_image_free": (None, [c_ubyte_p]),
+    "pt_image_write_png": (C.c_int, [C.c_char_p, C.c_int, C.c_int, c_ubyte_p, C.c_int]),
 }
 
 EXPORTED = tuple(_PROTOS)

@@ -23,7 +23,8 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "
           f"-I{INCLUDE}", f"-I{CSRC}"]
 
 HIP_SOURCES = ["pt_kernels.hip", "pt_wavefront.hip", "pt_runtime.cpp"]
-CXX_SOURCES = ["pt_host.cpp"]
+CXX_SOURCES = ["pt_host.cpp", "pt_loader.cpp", "pt_image.cpp"]
+LINK_LIBS = ["-lz"]  # zlib: PNG inflate/deflate (pt_image.cpp)
 
 
 def _hipcc() -> str:
@@ -69,7 +70,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
     tmp = LIB + ".tmp"
-    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp])
+    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, *LINK_LIBS, "-o", tmp])
     os.replace(tmp, LIB)
     return LIB
 

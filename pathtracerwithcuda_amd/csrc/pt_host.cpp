@@ -316,6 +316,205 @@ extern "C" void pt_bvh_free(pt_bvh_node_device* nodes, int* leaf_indices) {
     std::free(leaf_indices);
 }
 
+// ---- bvh_naive_cpu (Bvh/bvh.cpp:16-330): bucketed "SAH" split, then the same preorder flattening --
+namespace {
+
+struct GNode {
+    Box box;
+    int left = -1, right = -1, parent = -1;
+    bool leaf = false;
+    std::vector<int> tris;
+};
+
+inline float centroid_axis(const Box& b, int axis) { return 0.5f * (b.rt[axis] + b.lb[axis]); }
+inline void box_of_box(Box& dst, const Box& src) { dst = src; }
+inline float surface_area(const Box& b) {  // bounding_box::get_surface_area: 2 * volume (bounding_box.h:63-66)
+    return 2.0f * (b.rt[0] - b.lb[0]) * (b.rt[1] - b.lb[1]) * (b.rt[2] - b.lb[2]);
+}
+inline Box default_box() {  // bounding_box() (bounding_box.h:15-26)
+    Box b;
+    for (int k = 0; k < 3; k++) { b.lb[k] = -1.0f; b.rt[k] = -1.0f; }
+    return b;
+}
+// x86 cvttss2si: NaN and out-of-range values become INT_MIN (the reference's static_cast<int> of
+// (centroid - lb) / 0 on a zero-length axis)
+inline int trunc_to_int(float x) {
+    if (!(x >= -2147483648.0f && x < 2147483648.0f)) return (int)0x80000000u;
+    return (int)x;
+}
+
+void naive_split(std::vector<GNode>& nodes, const std::vector<Box>& boxes, int start, int leaf_size, int buckets_max) {
+    std::vector<int> stack{0};
+    std::vector<std::vector<int>> bucket_tris[3];
+    std::vector<Box> bucket_box[3];
+    std::vector<char> init(std::max(buckets_max, 1));
+    while (!stack.empty()) {
+        const int cur = stack.back();
+        stack.pop_back();
+        int split_axis = -1, split_i = 0, split_div = 0, nl = 0, nr = 0;
+        Box bl{}, br{};
+        float min_cost = INFINITY;
+        const std::vector<int> tris = nodes[(size_t)cur].tris;
+        const Box cbox = nodes[(size_t)cur].box;
+        for (int axis = 0; axis < 3; axis++) {
+            const float axis_length = cbox.rt[axis] - cbox.lb[axis];
+            const int div = std::min(buckets_max, (int)tris.size());
+            const float internal_length = axis_length / (float)div;
+            bucket_tris[axis].assign((size_t)div, {});
+            bucket_box[axis].assign((size_t)div, default_box());
+            std::fill(init.begin(), init.end(), 0);
+            for (int t : tris) {
+                const Box& tb = boxes[(size_t)(t - start)];
+                int k = trunc_to_int((centroid_axis(tb, axis) - cbox.lb[axis]) / internal_length);
+                k = k >= div ? div - 1 : (k < 0 ? 0 : k);
+                if (!init[k]) { box_of_box(bucket_box[axis][k], tb); init[k] = 1; }
+                else expand(bucket_box[axis][k], tb);
+                bucket_tris[axis][k].push_back(t);
+            }
+            for (int i = 0; i < div; i++) {
+                Box left = default_box(), right = default_box();
+                size_t cl = 0, cr = 0;
+                for (int j = 0; j < i; j++) if (init[j]) { box_of_box(left, bucket_box[axis][j]); break; }
+                for (int j = 0; j < i; j++)
+                    if (init[j]) { expand(left, bucket_box[axis][j]); cl += bucket_tris[axis][j].size(); }
+                for (int j = i; j < div; j++) if (init[j]) { box_of_box(right, bucket_box[axis][j]); break; }
+                for (int j = i; j < div; j++)
+                    if (init[j]) { expand(right, bucket_box[axis][j]); cr += bucket_tris[axis][j].size(); }
+                const float cost = surface_area(left) * (float)cl + surface_area(right) * (float)cr;
+                if (cost < min_cost && cost > 0.0f) {
+                    min_cost = cost; split_axis = axis; split_i = i; split_div = div;
+                    bl = left; br = right; nl = (int)cl; nr = (int)cr;
+                }
+            }
+        }
+        std::vector<int> lt, rt;
+        if (split_axis >= 0 && nl > 0 && nr > 0) {
+            for (int i = 0; i < split_i; i++)
+                lt.insert(lt.end(), bucket_tris[split_axis][i].begin(), bucket_tris[split_axis][i].end());
+            for (int i = split_i; i < split_div; i++)
+                rt.insert(rt.end(), bucket_tris[split_axis][i].begin(), bucket_tris[split_axis][i].end());
+        } else {
+            // No split with positive cost (planar geometry: every "surface area" is a zero volume), or a
+            // split that leaves one side empty: the reference then reads uninitialised split state or
+            // re-splits the same node forever. Defined here: halve the node's triangle list.
+            const size_t h = tris.size() / 2;
+            lt.assign(tris.begin(), tris.begin() + h);
+            rt.assign(tris.begin() + h, tris.end());
+            bl = boxes[(size_t)(lt[0] - start)];
+            for (int t : lt) expand(bl, boxes[(size_t)(t - start)]);
+            br = boxes[(size_t)(rt[0] - start)];
+            for (int t : rt) expand(br, boxes[(size_t)(t - start)]);
+        }
+        for (int side = 0; side < 2; side++) {
+            GNode child;
+            child.box = side == 0 ? bl : br;
+            child.tris = side == 0 ? lt : rt;
+            child.parent = cur;
+            child.leaf = (int)child.tris.size() <= leaf_size;
+            if (child.leaf) child.tris.resize((size_t)leaf_size, -1);
+            const int id = (int)nodes.size();
+            nodes.push_back(std::move(child));
+            (side == 0 ? nodes[(size_t)cur].left : nodes[(size_t)cur].right) = id;
+            if (!nodes[(size_t)id].leaf) stack.push_back(id);
+        }
+    }
+}
+
+// build_bvh_device_data (Bvh/bvh.cpp:244-330) over a linked tree rooted at node 0.
+int flatten_tree(std::vector<GNode>& nodes, int leaf_size, pt_bvh_node_device** nodes_out, int* node_num_out,
+                 int** leaf_out, int* leaf_num_out) {
+    std::vector<int> order, tindex(nodes.size(), -1);
+    {
+        std::vector<int> st{0};
+        while (!st.empty()) {
+            const int cur = st.back();
+            st.pop_back();
+            tindex[(size_t)cur] = (int)order.size();
+            order.push_back(cur);
+            GNode& g = nodes[(size_t)cur];
+            if (g.leaf && g.parent >= 0 && is_thin(g.box)) expand(g.box, nodes[(size_t)g.parent].box);
+            if (g.right != -1) st.push_back(g.right);
+            if (g.left != -1) st.push_back(g.left);
+        }
+    }
+    const int node_num = (int)order.size();
+    std::vector<int> next((size_t)node_num, node_num);
+    {
+        std::vector<int> st{0};
+        int k = 0;
+        while (!st.empty()) {
+            const int cur = st.back();
+            st.pop_back();
+            next[(size_t)k] = st.empty() ? node_num : tindex[(size_t)st.back()];
+            const GNode& g = nodes[(size_t)cur];
+            if (g.right != -1) st.push_back(g.right);
+            if (g.left != -1) st.push_back(g.left);
+            k++;
+        }
+    }
+    int leaves = 0;
+    for (int id : order) leaves += nodes[(size_t)id].leaf ? 1 : 0;
+    pt_bvh_node_device* out = (pt_bvh_node_device*)std::calloc((size_t)node_num, sizeof(pt_bvh_node_device));
+    int* slots = (int*)std::malloc((size_t)std::max(leaves, 1) * (size_t)leaf_size * sizeof(int));
+    if (!out || !slots) { std::free(out); std::free(slots); return -2; }
+    int li = 0;
+    for (int k = 0; k < node_num; k++) {
+        const GNode& g = nodes[(size_t)order[(size_t)k]];
+        pt_bvh_node_device& d = out[k];
+        d.box.left_bottom = {g.box.lb[0], g.box.lb[1], g.box.lb[2]};
+        d.box.right_top = {g.box.rt[0], g.box.rt[1], g.box.rt[2]};
+        d.box.centroid = {0.5f * (g.box.rt[0] + g.box.lb[0]), 0.5f * (g.box.rt[1] + g.box.lb[1]),
+                          0.5f * (g.box.rt[2] + g.box.lb[2])};
+        d.is_leaf = g.leaf ? 1 : 0;
+        d.next_node_index = next[(size_t)k];
+        d.triangle_indices = nullptr;
+        if (g.leaf) {
+            for (int j = 0; j < leaf_size; j++) slots[(size_t)li * leaf_size + j] = j < (int)g.tris.size() ? g.tris[(size_t)j] : -1;
+            d.triangle_indices = slots + (size_t)li * leaf_size;
+            li++;
+        }
+    }
+    *nodes_out = out;
+    *node_num_out = node_num;
+    *leaf_out = slots;
+    *leaf_num_out = li;
+    return 0;
+}
+
+}  // namespace
+
+// bvh_naive_cpu::build_bvh (Bvh/bvh.cpp:185-219) + build_bvh_device_data (:244-330).
+extern "C" int pt_bvh_build_naive(const pt_triangle* tris, int n, int start_index, int leaf_size, int bucket_num,
+                                  pt_bvh_node_device** nodes_out, int* node_num_out, int** leaf_out, int* leaf_num_out) {
+    if (!tris || n <= 0 || leaf_size <= 0 || bucket_num <= 0 || !nodes_out || !node_num_out || !leaf_out || !leaf_num_out)
+        return -1;
+    std::vector<GNode> nodes(1);
+    GNode& root = nodes[0];
+    root.box = box_of_triangle(tris[0]);
+    std::vector<Box> boxes((size_t)n);
+    for (int i = 0; i < n; i++) {
+        boxes[(size_t)i] = box_of_triangle(tris[i]);
+        expand(root.box, boxes[(size_t)i]);  // expand_to_fit_triangle
+        root.tris.push_back(i + start_index);
+    }
+    if ((int)root.tris.size() <= leaf_size) {
+        root.leaf = true;
+    } else {
+        naive_split(nodes, boxes, start_index, leaf_size, bucket_num);
+    }
+    return flatten_tree(nodes, leaf_size, nodes_out, node_num_out, leaf_out, leaf_num_out);
+}
+
+extern "C" int pt_bvh_build_ex(const pt_triangle* tris, int n, int start_index, int leaf_size, int method, int bucket_num,
+                               pt_bvh_node_device** nodes_out, int* node_num_out, int** leaf_out, int* leaf_num_out) {
+    if (method == PT_BVH_NAIVE_CPU)
+        return pt_bvh_build_naive(tris, n, start_index, leaf_size, bucket_num, nodes_out, node_num_out, leaf_out, leaf_num_out);
+    // MortonCodeCPU and MortonCodeCUDA build the same tree (Bvh/bvh.cpp:667-780 vs :862-1047); the
+    // CPU variant's std::sort is not stable, so equal codes keep their input order here as in the
+    // CUDA variant's merge sort.
+    return pt_bvh_build(tris, n, start_index, leaf_size, method, nodes_out, node_num_out, leaf_out, leaf_num_out);
+}
+
 // ---- scene assembly ----------------------------------------------------------------------------
 struct pt_scene_builder {
     std::vector<pt_material> materials;
@@ -365,35 +564,126 @@ extern "C" int pt_scene_builder_add_sphere(pt_scene_builder* b, pt_float3 center
 }
 
 namespace {
-// glm::rotate(m, angle, axis) = m * R(axis, angle) (glm/gtc/matrix_transform.inl)
-void rot_axis(double m[3][3], int axis, double deg) {
-    double a = deg * 3.14159265358979323846 / 180.0;
-    double c = std::cos(a), s = std::sin(a);
-    double r[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
-    int i = (axis + 1) % 3, j = (axis + 2) % 3;
-    r[i][i] = c; r[i][j] = -s; r[j][i] = s; r[j][j] = c;
-    double o[3][3];
-    for (int p = 0; p < 3; p++)
-        for (int q = 0; q < 3; q++) o[p][q] = m[p][0] * r[0][q] + m[p][1] * r[1][q] + m[p][2] * r[2][q];
-    std::memcpy(m, o, sizeof(o));
+// ---- glm 0.9.9 float matrices as the mesh loader uses them (lib/glm) ----------------------------
+// Column-major like glm: c[col][row]. Every expression keeps glm's evaluation order so that,
+// with contraction off, the transformed vertices and normals round as the reference's do.
+struct M4 {
+    float c[4][4];
+};
+M4 identity4() {
+    M4 m;
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) m.c[i][j] = i == j ? 1.0f : 0.0f;
+    return m;
 }
-inline pt_float3 norm3(double x, double y, double z) {
-    float fx = (float)x, fy = (float)y, fz = (float)z;
-    float inv = 1.0f / std::sqrt(fx * fx + fy * fy + fz * fz);
-    return {fx * inv, fy * inv, fz * inv};
+struct V4 {
+    float x, y, z, w;
+};
+inline V4 add4(V4 a, V4 b) { return {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+inline V4 mul4(V4 a, float s) { return {a.x * s, a.y * s, a.z * s, a.w * s}; }
+inline V4 mul4v(V4 a, V4 b) { return {a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w}; }
+inline V4 sub4(V4 a, V4 b) { return {a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w}; }
+inline V4 col(const M4& m, int i) { return {m.c[i][0], m.c[i][1], m.c[i][2], m.c[i][3]}; }
+inline void set_col(M4& m, int i, V4 v) { m.c[i][0] = v.x; m.c[i][1] = v.y; m.c[i][2] = v.z; m.c[i][3] = v.w; }
+
+// operator*(mat4, vec4) (glm/detail/type_mat4x4.inl:505-524): (m0*x + m1*y) + (m2*z + m3*w)
+V4 mat_vec(const M4& m, V4 v) {
+    return add4(add4(mul4(col(m, 0), v.x), mul4(col(m, 1), v.y)), add4(mul4(col(m, 2), v.z), mul4(col(m, 3), v.w)));
+}
+
+// glm::rotate (glm/gtc/matrix_transform.inl:18-47) about a unit coordinate axis
+M4 rotate4(const M4& m, float angle, int axis_index) {
+    const float c = std::cos(angle), s = std::sin(angle);
+    float axis[3] = {0.0f, 0.0f, 0.0f};
+    axis[axis_index] = 1.0f;  // normalize() of a unit axis is exact
+    const float temp[3] = {(1.0f - c) * axis[0], (1.0f - c) * axis[1], (1.0f - c) * axis[2]};
+    float R[3][3];
+    R[0][0] = c + temp[0] * axis[0];
+    R[0][1] = temp[0] * axis[1] + s * axis[2];
+    R[0][2] = temp[0] * axis[2] - s * axis[1];
+    R[1][0] = temp[1] * axis[0] - s * axis[2];
+    R[1][1] = c + temp[1] * axis[1];
+    R[1][2] = temp[1] * axis[2] + s * axis[0];
+    R[2][0] = temp[2] * axis[0] + s * axis[1];
+    R[2][1] = temp[2] * axis[1] - s * axis[0];
+    R[2][2] = c + temp[2] * axis[2];
+    M4 r;
+    for (int i = 0; i < 3; i++)
+        set_col(r, i, add4(add4(mul4(col(m, 0), R[i][0]), mul4(col(m, 1), R[i][1])), mul4(col(m, 2), R[i][2])));
+    set_col(r, 3, col(m, 3));
+    return r;
+}
+
+// glm::inverse, generic 4x4 path (glm/detail/func_matrix.inl:296-355)
+M4 inverse4(const M4& M) {
+    auto m = [&](int a, int b) { return M.c[a][b]; };
+    float c00 = m(2, 2) * m(3, 3) - m(3, 2) * m(2, 3), c02 = m(1, 2) * m(3, 3) - m(3, 2) * m(1, 3);
+    float c03 = m(1, 2) * m(2, 3) - m(2, 2) * m(1, 3);
+    float c04 = m(2, 1) * m(3, 3) - m(3, 1) * m(2, 3), c06 = m(1, 1) * m(3, 3) - m(3, 1) * m(1, 3);
+    float c07 = m(1, 1) * m(2, 3) - m(2, 1) * m(1, 3);
+    float c08 = m(2, 1) * m(3, 2) - m(3, 1) * m(2, 2), c10 = m(1, 1) * m(3, 2) - m(3, 1) * m(1, 2);
+    float c11 = m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2);
+    float c12 = m(2, 0) * m(3, 3) - m(3, 0) * m(2, 3), c14 = m(1, 0) * m(3, 3) - m(3, 0) * m(1, 3);
+    float c15 = m(1, 0) * m(2, 3) - m(2, 0) * m(1, 3);
+    float c16 = m(2, 0) * m(3, 2) - m(3, 0) * m(2, 2), c18 = m(1, 0) * m(3, 2) - m(3, 0) * m(1, 2);
+    float c19 = m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2);
+    float c20 = m(2, 0) * m(3, 1) - m(3, 0) * m(2, 1), c22 = m(1, 0) * m(3, 1) - m(3, 0) * m(1, 1);
+    float c23 = m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1);
+    V4 f0{c00, c00, c02, c03}, f1{c04, c04, c06, c07}, f2{c08, c08, c10, c11};
+    V4 f3{c12, c12, c14, c15}, f4{c16, c16, c18, c19}, f5{c20, c20, c22, c23};
+    V4 v0{m(1, 0), m(0, 0), m(0, 0), m(0, 0)}, v1{m(1, 1), m(0, 1), m(0, 1), m(0, 1)};
+    V4 v2{m(1, 2), m(0, 2), m(0, 2), m(0, 2)}, v3{m(1, 3), m(0, 3), m(0, 3), m(0, 3)};
+    V4 i0 = add4(sub4(mul4v(v1, f0), mul4v(v2, f1)), mul4v(v3, f2));
+    V4 i1 = add4(sub4(mul4v(v0, f0), mul4v(v2, f3)), mul4v(v3, f4));
+    V4 i2 = add4(sub4(mul4v(v0, f1), mul4v(v1, f3)), mul4v(v3, f5));
+    V4 i3 = add4(sub4(mul4v(v0, f2), mul4v(v1, f4)), mul4v(v2, f5));
+    const V4 sa{+1, -1, +1, -1}, sb{-1, +1, -1, +1};
+    M4 inv;
+    set_col(inv, 0, mul4v(i0, sa));
+    set_col(inv, 1, mul4v(i1, sb));
+    set_col(inv, 2, mul4v(i2, sa));
+    set_col(inv, 3, mul4v(i3, sb));
+    V4 row0{inv.c[0][0], inv.c[1][0], inv.c[2][0], inv.c[3][0]};
+    V4 dot0 = mul4v(col(M, 0), row0);
+    float dot1 = (dot0.x + dot0.y) + (dot0.z + dot0.w);
+    float one_over_det = 1.0f / dot1;
+    for (int i = 0; i < 4; i++) set_col(inv, i, mul4(col(inv, i), one_over_det));
+    return inv;
+}
+
+M4 transpose4(const M4& m) {
+    M4 t;
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) t.c[i][j] = m.c[j][i];
+    return t;
+}
+
+// normalize with the host rsqrtf = 1 / sqrtf (Math/cuda_math.hpp:33-36, :1458-1462)
+inline pt_float3 normalize_host(float x, float y, float z) {
+    const float inv = 1.0f / std::sqrt(x * x + y * y + z * z);
+    return {x * inv, y * inv, z * inv};
 }
 }  // namespace
 
-// triangle_mesh::load_obj (:136-171, rotation) + create_mesh_device_data (:593-647, translate*scale)
+// triangle_mesh::load_obj (:139-166): rotate Z, then Y, then X (glm::radians degrees), normals by the
+// inverse transpose, renormalised; then create_mesh_device_data (:625-647): translate * scale, normals
+// by its inverse transpose, renormalised.
 extern "C" int pt_scene_builder_add_mesh(pt_scene_builder* b, int tri_num, const float* v, const float* nrm,
                                          const float* uv, const int* tri_material, pt_float3 pos, pt_float3 scl,
                                          pt_float3 rot) {
     if (!b || tri_num <= 0 || !v || !nrm || !tri_material) return -1;
-    double R[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
-    rot_axis(R, 2, rot.z);
-    rot_axis(R, 1, rot.y);
-    rot_axis(R, 0, rot.x);
-    const bool identity = rot.x == 0.0f && rot.y == 0.0f && rot.z == 0.0f;
+    const float deg = 0.01745329251994329576923690768489f;  // glm::radians
+    M4 R = identity4();
+    R = rotate4(R, rot.z * deg, 2);
+    R = rotate4(R, rot.y * deg, 1);
+    R = rotate4(R, rot.x * deg, 0);
+    const M4 Rn = transpose4(inverse4(R));
+    M4 T = identity4();  // glm::translate(I, pos) then glm::scale(., scl)
+    set_col(T, 3, add4(add4(add4(mul4(col(T, 0), pos.x), mul4(col(T, 1), pos.y)), mul4(col(T, 2), pos.z)), col(T, 3)));
+    set_col(T, 0, mul4(col(T, 0), scl.x));
+    set_col(T, 1, mul4(col(T, 1), scl.y));
+    set_col(T, 2, mul4(col(T, 2), scl.z));
+    const M4 Tn = transpose4(inverse4(T));
     b->mesh_start.push_back((int)b->triangles.size());
     b->mesh_count.push_back(tri_num);
     for (int t = 0; t < tri_num; t++) {
@@ -405,23 +695,13 @@ extern "C" int pt_scene_builder_add_mesh(pt_scene_builder* b, int tri_num, const
         for (int k = 0; k < 3; k++) {
             const float* p = v + (size_t)t * 9 + k * 3;
             const float* q = nrm + (size_t)t * 9 + k * 3;
-            float rx, ry, rz;
-            double nx, ny, nz;
-            if (identity) {
-                rx = p[0]; ry = p[1]; rz = p[2];
-                nx = q[0]; ny = q[1]; nz = q[2];
-            } else {
-                rx = (float)(R[0][0] * p[0] + R[0][1] * p[1] + R[0][2] * p[2]);
-                ry = (float)(R[1][0] * p[0] + R[1][1] * p[1] + R[1][2] * p[2]);
-                rz = (float)(R[2][0] * p[0] + R[2][1] * p[1] + R[2][2] * p[2]);
-                nx = R[0][0] * q[0] + R[0][1] * q[1] + R[0][2] * q[2];
-                ny = R[1][0] * q[0] + R[1][1] * q[1] + R[1][2] * q[2];
-                nz = R[2][0] * q[0] + R[2][1] * q[1] + R[2][2] * q[2];
-            }
-            pt_float3 nr = norm3(nx, ny, nz);  // normalize after rotation (:163-165)
-            *vo[k] = {scl.x * rx + pos.x, scl.y * ry + pos.y, scl.z * rz + pos.z};
-            // inverse transpose of translate*scale on a direction = diag(1/s) (:633-644)
-            *no[k] = norm3((double)(nr.x / scl.x), (double)(nr.y / scl.y), (double)(nr.z / scl.z));
+            const V4 rv = mat_vec(R, V4{p[0], p[1], p[2], 1.0f});
+            const V4 rn = mat_vec(Rn, V4{q[0], q[1], q[2], 0.0f});
+            const pt_float3 n1 = normalize_host(rn.x, rn.y, rn.z);
+            const V4 wv = mat_vec(T, V4{rv.x, rv.y, rv.z, 1.0f});
+            const V4 wn = mat_vec(Tn, V4{n1.x, n1.y, n1.z, 0.0f});
+            *vo[k] = {wv.x, wv.y, wv.z};
+            *no[k] = normalize_host(wn.x, wn.y, wn.z);
             if (uv) *uo[k] = {uv[(size_t)t * 6 + k * 2], uv[(size_t)t * 6 + k * 2 + 1]};
             else *uo[k] = {0.0f, 0.0f};
         }
@@ -450,6 +730,10 @@ extern "C" int pt_scene_builder_add_texture(pt_scene_builder* b, int w, int h, c
 }
 
 extern "C" int pt_scene_builder_build(pt_scene_builder* b, int leaf_size, int method) {
+    return pt_scene_builder_build_ex(b, leaf_size, method, 12);
+}
+
+extern "C" int pt_scene_builder_build_ex(pt_scene_builder* b, int leaf_size, int method, int bucket_num) {
     if (!b) return -1;
     b->release_bvh();
     for (size_t t = 0; t < b->triangles.size(); t++) {
@@ -460,8 +744,8 @@ extern "C" int pt_scene_builder_build(pt_scene_builder* b, int leaf_size, int me
     for (size_t m = 0; m < b->mesh_start.size(); m++) {
         pt_bvh_node_device* nodes = nullptr;
         int nn = 0, *leaf = nullptr, ln = 0;
-        int rc = pt_bvh_build(b->triangles.data() + b->mesh_start[m], b->mesh_count[m], b->mesh_start[m], leaf_size,
-                              method, &nodes, &nn, &leaf, &ln);
+        int rc = pt_bvh_build_ex(b->triangles.data() + b->mesh_start[m], b->mesh_count[m], b->mesh_start[m], leaf_size,
+                                 method, bucket_num, &nodes, &nn, &leaf, &ln);
         if (rc != 0) return rc;
         b->bvh_nodes.push_back(nodes);
         b->bvh_leaf.push_back(leaf);
