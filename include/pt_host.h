@@ -81,6 +81,9 @@ int pt_scene_builder_add_texture(pt_scene_builder* b, int width, int height, con
 /* Builds every mesh BVH and fixes up the embedded pointers. */
 int pt_scene_builder_build(pt_scene_builder* b, int leaf_size, int method);
 int pt_scene_builder_build_ex(pt_scene_builder* b, int leaf_size, int method, int bucket_num);
+/* Where MortonCodeCUDA builds run: -2 (default) the current HIP device when one is present, else the
+ * host builder (identical output); -1 always the host; >= 0 the HIP device (include/pt_bvh.h). */
+int pt_scene_builder_set_bvh_device(pt_scene_builder* b, int device);
 int pt_scene_builder_view(pt_scene_builder* b, pt_scene_view* out);
 
 /* ---- camera (Core/camera.cpp) --------------------------------------------------------------- */

@@ -98,6 +98,20 @@ typedef struct pt_bvh_node_device {
     int next_node_index;
 } pt_bvh_node_device;
 
+/* Bvh/bvh_node.h:27-39 ; the Morton/CUDA builder's intermediate node (64 B) */
+typedef struct pt_bvh_node_morton_code_cuda {
+    pt_bounding_box box;
+    int left_index;
+    int right_index;
+    int parent_index;
+    unsigned char is_left_leaf;
+    unsigned char is_right_leaf;
+    unsigned char is_leaf;
+    int triangle_index;
+    unsigned int morton_code;
+    int is_visited;
+} pt_bvh_node_morton_code_cuda;
+
 /* Core/camera.h:14-23 */
 typedef struct pt_render_camera {
     pt_float3 eye;
@@ -185,6 +199,9 @@ PT_STATIC_ASSERT(offsetof(pt_triangle, mat) == 96, "triangle.mat");
 PT_STATIC_ASSERT(sizeof(pt_bvh_node_device) == 56, "bvh_node_device layout");
 PT_STATIC_ASSERT(offsetof(pt_bvh_node_device, triangle_indices) == 40, "bvh_node.triangle_indices");
 PT_STATIC_ASSERT(offsetof(pt_bvh_node_device, next_node_index) == 52, "bvh_node.next");
+PT_STATIC_ASSERT(sizeof(pt_bvh_node_morton_code_cuda) == 64, "bvh_node_morton_code_cuda layout");
+PT_STATIC_ASSERT(offsetof(pt_bvh_node_morton_code_cuda, is_left_leaf) == 48, "morton_node.is_left_leaf");
+PT_STATIC_ASSERT(offsetof(pt_bvh_node_morton_code_cuda, triangle_index) == 52, "morton_node.triangle_index");
 PT_STATIC_ASSERT(sizeof(pt_render_camera) == 64, "render_camera layout");
 PT_STATIC_ASSERT(offsetof(pt_render_camera, resolution) == 40, "render_camera.resolution");
 PT_STATIC_ASSERT(sizeof(pt_configuration) == 96, "configuration layout");

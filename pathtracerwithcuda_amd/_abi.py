@@ -81,6 +81,14 @@ class BvhNodeDevice(C.Structure):  # Bvh/bvh_node.h:41-47
     ]
 
 
+class BvhNodeMorton(C.Structure):  # Bvh/bvh_node.h:27-39 (bvh_node_morton_code_cuda)
+    _fields_ = [
+        ("box", BoundingBox), ("left_index", C.c_int), ("right_index", C.c_int), ("parent_index", C.c_int),
+        ("is_left_leaf", C.c_ubyte), ("is_right_leaf", C.c_ubyte), ("is_leaf", C.c_ubyte),
+        ("triangle_index", C.c_int), ("morton_code", C.c_uint), ("is_visited", C.c_int),
+    ]
+
+
 class RenderCamera(C.Structure):  # Core/camera.h:14-23
     _fields_ = [
         ("eye", Float3), ("view", Float3), ("up", Float3), ("_pad", C.c_uint32),
@@ -158,7 +166,7 @@ class SceneLoadOptions(C.Structure):  # include/pt_loader.h
 
 LAYOUT = {  # include/pt_types.h static asserts
     "Ray": 24, "Scattering": 24, "Medium": 32, "Material": 84, "Sphere": 100, "Triangle": 104,
-    "BoundingBox": 36, "BvhNodeDevice": 56, "RenderCamera": 64, "Configuration": 96, "CubeMap": 56,
+    "BoundingBox": 36, "BvhNodeDevice": 56, "BvhNodeMorton": 64, "RenderCamera": 64, "Configuration": 96, "CubeMap": 56,
     "TextureWrapper": 16,
 }
 
@@ -225,6 +233,13 @@ _PROTOS = {
     "pt_bvh_build_naive": (C.c_int, [C.POINTER(Triangle), C.c_int, C.c_int, C.c_int, C.c_int,
                                      C.POINTER(C.POINTER(BvhNodeDevice)), c_int_p, C.POINTER(c_int_p), c_int_p]),
     "pt_scene_builder_build_ex": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
+    "pt_scene_builder_set_bvh_device": (C.c_int, [C.c_void_p, C.c_int]),
+    # GPU BVH builder (include/pt_bvh.h)
+    "compute_triangle_bounding_box_kernel": (None, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
+    "generate_internal_node_kernel": (None, [C.c_void_p, C.c_uint, C.c_void_p, C.c_uint, C.c_int]),
+    "radix_sort": (None, [C.c_void_p, C.c_void_p, C.c_int]),
+    "pt_bvh_build_device": (C.c_int, [C.POINTER(Triangle), C.c_int, C.c_int, C.c_int,
+                                      C.POINTER(C.POINTER(BvhNodeDevice)), c_int_p, C.POINTER(c_int_p), c_int_p]),
     # ingestion (include/pt_loader.h)
     "pt_config_load": (C.c_int, [C.c_char_p, C.POINTER(Configuration)]),
     "pt_material_preset": (C.c_int, [C.c_char_p, C.POINTER(Material)]),

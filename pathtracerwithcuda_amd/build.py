@@ -22,7 +22,7 @@ ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
           f"-I{INCLUDE}", f"-I{CSRC}"]
 
-HIP_SOURCES = ["pt_kernels.hip", "pt_wavefront.hip", "pt_runtime.cpp"]
+HIP_SOURCES = ["pt_kernels.hip", "pt_wavefront.hip", "pt_bvh.hip", "pt_runtime.cpp"]
 CXX_SOURCES = ["pt_host.cpp", "pt_loader.cpp", "pt_image.cpp"]
 LINK_LIBS = ["-lz"]  # zlib: PNG inflate/deflate (pt_image.cpp)
 

@@ -1,0 +1,29 @@
+// pt_bvh_internal.h — the hand-off between the Morton builders' first half (host: pt_host.cpp,
+// device: pt_bvh.hip) and their shared second half (pt_morton_finish in pt_host.cpp).
+#pragma once
+
+#include <vector>
+
+#include "../../include/pt_types.h"
+#include "pt_bvh_common.h"
+
+// Sorted leaves and the Karras internal nodes of one mesh (Bvh/bvh.cpp:862-972).
+struct PtMortonTree {
+    unsigned int leaf_num = 0, internal_num = 0;
+    std::vector<ptbvh::Box> leaf_box;  // leaves in Morton order
+    std::vector<int> leaf_batch;       // batch of each sorted leaf (index into batch_tris / leaf_size)
+    std::vector<int> batch_tris;       // leaf_num * leaf_size triangle ids, -1 padded
+    std::vector<int> inner_left, inner_right;  // child: >= 0 internal id, <= -2 leaf -(id + 2)
+    std::vector<int> inner_parent, leaf_parent;  // -1 = none
+};
+
+// leaf count of bvh.cpp:866-868
+inline unsigned int pt_leaf_count(int n, int leaf_size) {
+    unsigned int l = (unsigned int)(n / leaf_size);
+    l = l == 0 ? 1 : l;
+    return (n % leaf_size == 0) ? l : l + 1;
+}
+
+// Bottom-up boxes and the flattened skip-pointer array (Bvh/bvh.cpp:974-1047, :244-330).
+int pt_morton_finish(PtMortonTree& t, int leaf_size, pt_bvh_node_device** nodes_out, int* node_num_out,
+                     int** leaf_out, int* leaf_num_out);

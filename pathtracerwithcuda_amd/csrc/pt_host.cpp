@@ -7,201 +7,45 @@
 #include <vector>
 
 #include "../../include/pt_host.h"
+#include "pt_bvh_common.h"
+#include "pt_bvh_internal.h"
+#include "../../include/pt_bvh.h"
+#include "../../include/pt_native.h"
 
 namespace {
 
-// ---- Bvh/bounding_box.h ------------------------------------------------------------------------
-struct Box {
-    float lb[3], rt[3];
-};
+using ptbvh::Box;
+using ptbvh::expand;
+using ptbvh::is_thin;
 
 inline Box box_of_triangle(const pt_triangle& t) {  // bounding_box::get_bounding_box(v0, v1, v2)
-    Box b;
-    const float* v0 = &t.vertex0.x;
-    const float* v1 = &t.vertex1.x;
-    const float* v2 = &t.vertex2.x;
-    for (int k = 0; k < 3; k++) {
-        float mn = v0[k], mx = v0[k];
-        // cuda_math.hpp min(a,b,c) / max(a,b,c): sequential compares
-        mn = v1[k] < mn ? v1[k] : mn; mn = v2[k] < mn ? v2[k] : mn;
-        mx = v1[k] > mx ? v1[k] : mx; mx = v2[k] > mx ? v2[k] : mx;
-        b.lb[k] = mn; b.rt[k] = mx;
-    }
-    return b;
+    return ptbvh::box_of_vertices(&t.vertex0.x, &t.vertex1.x, &t.vertex2.x);
 }
-
-inline void expand(Box& a, const Box& b) {  // expand_to_fit_box: fminf / fmaxf
-    for (int k = 0; k < 3; k++) {
-        a.lb[k] = std::fmin(a.lb[k], b.lb[k]);
-        a.rt[k] = std::fmax(a.rt[k], b.rt[k]);
-    }
-}
-
-inline bool is_thin(const Box& b) {  // bounding_box::is_thin_bounding_box
-    return b.rt[0] == b.lb[0] || b.rt[1] == b.lb[1] || b.rt[2] == b.lb[2];
-}
-
-// ---- Bvh/bvh.cpp:370-392 -----------------------------------------------------------------------
-inline unsigned int expand_bits(unsigned int v) {
-    v = (v * 0x00010001u) & 0xFF0000FFu;
-    v = (v * 0x00000101u) & 0x0F00F00Fu;
-    v = (v * 0x00000011u) & 0xC30C30C3u;
-    v = (v * 0x00000005u) & 0x49249249u;
-    return v;
-}
-
-inline unsigned int morton(float px, float py, float pz) {
-    // fminf(fmaxf(p*1024, 0), 1023): a NaN coordinate (zero mesh extent) maps to 0
-    float x = std::fmin(std::fmax(px * 1024.0f, 0.0f), 1023.0f);
-    float y = std::fmin(std::fmax(py * 1024.0f, 0.0f), 1023.0f);
-    float z = std::fmin(std::fmax(pz * 1024.0f, 0.0f), 1023.0f);
-    return expand_bits((unsigned int)x) * 4 + expand_bits((unsigned int)y) * 2 + expand_bits((unsigned int)z);
-}
-
-inline unsigned int morton_of_box(const Box& b, const Box& mesh) {
-    // (centroid - mesh.lb) / (mesh.rt - mesh.lb), centroid = 0.5 * (rt + lb)
-    float c[3], p[3];
-    for (int k = 0; k < 3; k++) {
-        c[k] = 0.5f * (b.rt[k] + b.lb[k]);
-        p[k] = (c[k] - mesh.lb[k]) / (mesh.rt[k] - mesh.lb[k]);
-    }
-    return morton(p[0], p[1], p[2]);
-}
-
-// Bvh/bvh.cpp:398-441 (table-driven; equals __builtin_clz with clz(0) = 32)
-inline unsigned int clz32(unsigned int v) { return v == 0 ? 32u : (unsigned int)__builtin_clz(v); }
-
-// Bvh/bvh.cpp:446-481
-unsigned int find_split(const std::vector<unsigned int>& code, unsigned int first, unsigned int last) {
-    unsigned int fc = code[first], lc = code[last];
-    if (fc == lc) return first;
-    unsigned int common = clz32(fc ^ lc);
-    unsigned int split = first;
-    unsigned int step = last - first;
-    do {
-        step = (step + 1) >> 1;
-        unsigned int ns = split + step;
-        if (ns < last) {
-            if (clz32(fc ^ code[ns]) > common) split = ns;
-        }
-    } while (step > 1);
-    return split;
-}
-
-// Bvh/bvh.cpp:486-570, including its unsigned wrap-around and the equal-code run handling.
-void find_range(const std::vector<unsigned int>& code, unsigned int n, unsigned int index,
-                unsigned int* rx, unsigned int* ry) {
-    if (index == 0) { *rx = 0; *ry = n - 1; return; }
-    unsigned int initial = index;
-    unsigned int prev = code[index - 1], cur = code[index], next = code[index + 1];
-    int direction;
-    unsigned int delta_min;
-    if (prev == cur && cur == next) {
-        while (index > 0 && index < n - 1) {
-            index++;
-            if (index >= n - 1) break;
-            if (code[index] != code[index + 1]) break;
-        }
-        *rx = initial; *ry = index;
-        return;
-    }
-    unsigned int left = clz32(cur ^ prev), right = clz32(cur ^ next);
-    if (left > right) { direction = -1; delta_min = right; }
-    else { direction = 1; delta_min = left; }
-    unsigned int l_max = 2;
-    unsigned int test = index + l_max * (unsigned int)direction;
-    while (test < n && clz32(cur ^ code[test]) > delta_min) {
-        l_max *= 2;
-        test = index + l_max * (unsigned int)direction;
-    }
-    int l = 0;
-    for (int divisor = 2; l_max / (unsigned int)divisor >= 1; divisor *= 2) {
-        int t = (int)(l_max / (unsigned int)divisor);
-        test = index + (unsigned int)((l + t) * direction);
-        if (test < n) {
-            if (clz32(cur ^ code[test]) > delta_min) l = l + t;
-        }
-    }
-    if (direction == 1) { *rx = index; *ry = index + (unsigned int)(l * direction); }
-    else { *rx = index + (unsigned int)(l * direction); *ry = index; }
-}
-
-struct BuildNode {
-    Box box;
-    int left = -1, right = -1;   // child ids: >= 0 internal, <= -2 leaf (-(leaf+2))
-    int parent = -1;             // internal id
-};
 
 }  // namespace
 
-extern "C" unsigned int pt_morton_code(float x, float y, float z) { return morton(x, y, z); }
-extern "C" unsigned int pt_clz_table(unsigned int value) { return clz32(value); }
+extern "C" unsigned int pt_morton_code(float x, float y, float z) { return ptbvh::morton(x, y, z); }
+extern "C" unsigned int pt_clz_table(unsigned int value) { return ptbvh::clz32(value); }
 
-// bvh_morton_code_cuda::build_bvh (Bvh/bvh.cpp:862-1047) + bvh_naive_cpu::build_bvh_device_data
-// (:244-330). thrust::sort with a comparator is a stable merge sort, so std::stable_sort.
-extern "C" int pt_bvh_build(const pt_triangle* tris, int n, int start_index, int leaf_size, int method,
-                            pt_bvh_node_device** nodes_out, int* node_num_out, int** leaf_out, int* leaf_num_out) {
-    (void)method;  // the Morton builder for every method (naive-SAH builder is a later row)
-    if (!tris || n <= 0 || leaf_size <= 0 || !nodes_out || !node_num_out || !leaf_out || !leaf_num_out) return -1;
-
-    unsigned int leaf_num = (unsigned int)(n / leaf_size);
-    leaf_num = leaf_num == 0 ? 1 : leaf_num;
-    leaf_num = (n % leaf_size == 0) ? leaf_num : leaf_num + 1;
-    const unsigned int internal_num = leaf_num - 1;
-
-    // mesh box (:889-895)
-    Box mesh = box_of_triangle(tris[0]);
-    for (int i = 1; i < n; i++) {
-        Box b = box_of_triangle(tris[i]);
-        expand(mesh, b);
-    }
-
-    // per-triangle box + Morton code (bvh_morton_code_kernel.cu:298-326)
-    struct TriNode { Box box; unsigned int code; int tri; };
-    std::vector<TriNode> tn((size_t)n);
-    for (int i = 0; i < n; i++) {
-        tn[i].box = box_of_triangle(tris[i]);
-        tn[i].code = morton_of_box(tn[i].box, mesh);
-        tn[i].tri = i + start_index;
-    }
-    std::stable_sort(tn.begin(), tn.end(), [](const TriNode& a, const TriNode& b) { return a.code < b.code; });
-
-    // batch into leaves (:920-955), then sort the leaves by the code of their own box
-    struct LeafNode { Box box; unsigned int code; int batch; };
-    std::vector<LeafNode> leaves(leaf_num);
-    std::vector<int> batch_tris((size_t)leaf_num * leaf_size, -1);
-    for (unsigned int i = 0; i < leaf_num; i++) {
-        int s = (int)i * leaf_size;
-        leaves[i].box = tn[s].box;
-        batch_tris[(size_t)i * leaf_size] = tn[s].tri;
-        for (int j = 1; j < leaf_size; j++) {
-            if (j + s < n) {
-                expand(leaves[i].box, tn[j + s].box);
-                batch_tris[(size_t)i * leaf_size + j] = tn[j + s].tri;
-            }
-        }
-        leaves[i].code = morton_of_box(leaves[i].box, mesh);
-        leaves[i].batch = (int)i;
-    }
-    std::stable_sort(leaves.begin(), leaves.end(), [](const LeafNode& a, const LeafNode& b) { return a.code < b.code; });
-
-    // Karras internal nodes (bvh_morton_code_kernel.cu:262-296), sequential in index order
-    std::vector<unsigned int> codes(leaf_num);
-    for (unsigned int i = 0; i < leaf_num; i++) codes[i] = leaves[i].code;
+// The second half of bvh_morton_code_cuda::build_bvh (Bvh/bvh.cpp:974-1047) and
+// bvh_naive_cpu::build_bvh_device_data (:244-330), shared by the host and the device builder
+// (pt_bvh_internal.h): bottom-up boxes, then the preorder skip-pointer array.
+int pt_morton_finish(PtMortonTree& t, int leaf_size, pt_bvh_node_device** nodes_out, int* node_num_out,
+                     int** leaf_out, int* leaf_num_out) {
+    const unsigned int leaf_num = t.leaf_num, internal_num = t.internal_num;
+    struct BuildNode {
+        Box box;
+        int left, right, parent;
+    };
     std::vector<BuildNode> inner(internal_num);
-    std::vector<int> leaf_parent(leaf_num, -1);
     for (unsigned int i = 0; i < internal_num; i++) {
-        unsigned int rx, ry;
-        find_range(codes, leaf_num, i, &rx, &ry);
-        unsigned int split = find_split(codes, rx, ry);
-        if (split == rx) { inner[i].left = -((int)split + 2); leaf_parent[split] = (int)i; }
-        else { inner[i].left = (int)split; inner[split].parent = (int)i; }
-        if (split + 1 == ry) { inner[i].right = -((int)(split + 1) + 2); leaf_parent[split + 1] = (int)i; }
-        else { inner[i].right = (int)(split + 1); inner[split + 1].parent = (int)i; }
+        inner[i].left = t.inner_left[i];
+        inner[i].right = t.inner_right[i];
+        inner[i].parent = t.inner_parent[i];
     }
-
+    std::vector<Box>& leaf_box = t.leaf_box;
     // bottom-up boxes: union of the two children (:817-860), post-order from the root
-    auto child_box = [&](int c) -> const Box& { return c <= -2 ? leaves[(size_t)(-c - 2)].box : inner[(size_t)c].box; };
+    auto child_box = [&](int c) -> const Box& { return c <= -2 ? leaf_box[(size_t)(-c - 2)] : inner[(size_t)c].box; };
     if (internal_num > 0) {
         std::vector<std::pair<int, int>> st;
         st.reserve(64);
@@ -227,8 +71,8 @@ extern "C" int pt_bvh_build(const pt_triangle* tris, int n, int start_index, int
 
     // flatten: preorder with an explicit stack, right pushed before left (:244-330)
     struct Ref { int id; bool leaf; };
-    auto node_box = [&](Ref r) -> Box& { return r.leaf ? leaves[(size_t)r.id].box : inner[(size_t)r.id].box; };
-    auto parent_of = [&](Ref r) -> int { return r.leaf ? leaf_parent[(size_t)r.id] : inner[(size_t)r.id].parent; };
+    auto node_box = [&](Ref r) -> Box& { return r.leaf ? leaf_box[(size_t)r.id] : inner[(size_t)r.id].box; };
+    auto parent_of = [&](Ref r) -> int { return r.leaf ? t.leaf_parent[(size_t)r.id] : inner[(size_t)r.id].parent; };
     std::vector<Ref> order;
     order.reserve((size_t)leaf_num + internal_num);
     {
@@ -254,7 +98,6 @@ extern "C" int pt_bvh_build(const pt_triangle* tris, int n, int start_index, int
     const int node_num = (int)order.size();
     std::vector<int> next_index((size_t)node_num, node_num);
     {
-        // traversal index of each (leaf/internal id)
         std::vector<int> tidx_inner(internal_num, -1), tidx_leaf(leaf_num, -1);
         for (int k = 0; k < node_num; k++) {
             if (order[(size_t)k].leaf) tidx_leaf[(size_t)order[(size_t)k].id] = k;
@@ -267,8 +110,8 @@ extern "C" int pt_bvh_build(const pt_triangle* tris, int n, int start_index, int
             Ref cur = st.back();
             st.pop_back();
             if (!st.empty()) {
-                Ref t = st.back();
-                next_index[(size_t)k] = t.leaf ? tidx_leaf[(size_t)t.id] : tidx_inner[(size_t)t.id];
+                Ref top = st.back();
+                next_index[(size_t)k] = top.leaf ? tidx_leaf[(size_t)top.id] : tidx_inner[(size_t)top.id];
             } else {
                 next_index[(size_t)k] = node_num;
             }
@@ -298,8 +141,8 @@ extern "C" int pt_bvh_build(const pt_triangle* tris, int n, int start_index, int
         d.next_node_index = next_index[(size_t)k];
         d.triangle_indices = nullptr;
         if (r.leaf) {
-            int batch = leaves[(size_t)r.id].batch;
-            for (int j = 0; j < leaf_size; j++) leaf_idx[(size_t)li * leaf_size + j] = batch_tris[(size_t)batch * leaf_size + j];
+            int batch = t.leaf_batch[(size_t)r.id];
+            for (int j = 0; j < leaf_size; j++) leaf_idx[(size_t)li * leaf_size + j] = t.batch_tris[(size_t)batch * leaf_size + j];
             d.triangle_indices = leaf_idx + (size_t)li * leaf_size;
             li++;
         }
@@ -309,6 +152,76 @@ extern "C" int pt_bvh_build(const pt_triangle* tris, int n, int start_index, int
     *leaf_out = leaf_idx;
     *leaf_num_out = li;
     return 0;
+}
+
+// bvh_morton_code_cuda::build_bvh (Bvh/bvh.cpp:862-1047) + bvh_naive_cpu::build_bvh_device_data
+// (:244-330), all on the host. thrust::sort with a comparator is a stable merge sort, so std::stable_sort.
+extern "C" int pt_bvh_build(const pt_triangle* tris, int n, int start_index, int leaf_size, int method,
+                            pt_bvh_node_device** nodes_out, int* node_num_out, int** leaf_out, int* leaf_num_out) {
+    (void)method;
+    if (!tris || n <= 0 || leaf_size <= 0 || !nodes_out || !node_num_out || !leaf_out || !leaf_num_out) return -1;
+
+    PtMortonTree t;
+    t.leaf_num = pt_leaf_count(n, leaf_size);
+    t.internal_num = t.leaf_num - 1;
+
+    // mesh box (:889-895)
+    Box mesh = box_of_triangle(tris[0]);
+    for (int i = 1; i < n; i++) expand(mesh, box_of_triangle(tris[i]));
+
+    // per-triangle box + Morton code (bvh_morton_code_kernel.cu:298-326)
+    struct TriNode { Box box; unsigned int code; int tri; };
+    std::vector<TriNode> tn((size_t)n);
+    for (int i = 0; i < n; i++) {
+        tn[i].box = box_of_triangle(tris[i]);
+        tn[i].code = ptbvh::morton_of_box(tn[i].box, mesh);
+        tn[i].tri = i + start_index;
+    }
+    std::stable_sort(tn.begin(), tn.end(), [](const TriNode& a, const TriNode& b) { return a.code < b.code; });
+
+    // batch into leaves (:920-955), then sort the leaves by the code of their own box
+    struct LeafNode { Box box; unsigned int code; int batch; };
+    std::vector<LeafNode> leaves(t.leaf_num);
+    t.batch_tris.assign((size_t)t.leaf_num * leaf_size, -1);
+    for (unsigned int i = 0; i < t.leaf_num; i++) {
+        int s = (int)i * leaf_size;
+        leaves[i].box = tn[s].box;
+        t.batch_tris[(size_t)i * leaf_size] = tn[s].tri;
+        for (int j = 1; j < leaf_size; j++) {
+            if (j + s < n) {
+                expand(leaves[i].box, tn[j + s].box);
+                t.batch_tris[(size_t)i * leaf_size + j] = tn[j + s].tri;
+            }
+        }
+        leaves[i].code = ptbvh::morton_of_box(leaves[i].box, mesh);
+        leaves[i].batch = (int)i;
+    }
+    std::stable_sort(leaves.begin(), leaves.end(), [](const LeafNode& a, const LeafNode& b) { return a.code < b.code; });
+
+    // Karras internal nodes (bvh_morton_code_kernel.cu:262-296), sequential in index order: the
+    // last writer of a parent link is the largest internal index
+    std::vector<unsigned int> codes(t.leaf_num);
+    t.leaf_box.resize(t.leaf_num);
+    t.leaf_batch.resize(t.leaf_num);
+    for (unsigned int i = 0; i < t.leaf_num; i++) {
+        codes[i] = leaves[i].code;
+        t.leaf_box[i] = leaves[i].box;
+        t.leaf_batch[i] = leaves[i].batch;
+    }
+    t.inner_left.assign(t.internal_num, -1);
+    t.inner_right.assign(t.internal_num, -1);
+    t.inner_parent.assign(t.internal_num, -1);
+    t.leaf_parent.assign(t.leaf_num, -1);
+    for (unsigned int i = 0; i < t.internal_num; i++) {
+        unsigned int rx, ry;
+        ptbvh::find_range(codes, t.leaf_num, i, &rx, &ry);
+        unsigned int split = ptbvh::find_split(codes, rx, ry);
+        if (split == rx) { t.inner_left[i] = -((int)split + 2); t.leaf_parent[split] = (int)i; }
+        else { t.inner_left[i] = (int)split; t.inner_parent[split] = (int)i; }
+        if (split + 1 == ry) { t.inner_right[i] = -((int)(split + 1) + 2); t.leaf_parent[split + 1] = (int)i; }
+        else { t.inner_right[i] = (int)(split + 1); t.inner_parent[split + 1] = (int)i; }
+    }
+    return pt_morton_finish(t, leaf_size, nodes_out, node_num_out, leaf_out, leaf_num_out);
 }
 
 extern "C" void pt_bvh_free(pt_bvh_node_device* nodes, int* leaf_indices) {
@@ -533,6 +446,7 @@ struct pt_scene_builder {
     std::vector<pt_texture_wrapper> tex_wrappers;
     pt_cube_map cube_map{};
     bool built = false;
+    int bvh_device = -2;  // MortonCodeCUDA builds on: -2 the HIP device when one is present, -1 the host, >= 0 the device
 
     void release_bvh() {
         for (size_t i = 0; i < bvh_nodes.size(); i++) pt_bvh_free(bvh_nodes[i], bvh_leaf[i]);
@@ -733,6 +647,13 @@ extern "C" int pt_scene_builder_build(pt_scene_builder* b, int leaf_size, int me
     return pt_scene_builder_build_ex(b, leaf_size, method, 12);
 }
 
+extern "C" int pt_scene_builder_set_bvh_device(pt_scene_builder* b, int device) {
+    if (!b || device < -2) return -1;
+    b->bvh_device = device;
+    b->built = false;
+    return 0;
+}
+
 extern "C" int pt_scene_builder_build_ex(pt_scene_builder* b, int leaf_size, int method, int bucket_num) {
     if (!b) return -1;
     b->release_bvh();
@@ -744,8 +665,14 @@ extern "C" int pt_scene_builder_build_ex(pt_scene_builder* b, int leaf_size, int
     for (size_t m = 0; m < b->mesh_start.size(); m++) {
         pt_bvh_node_device* nodes = nullptr;
         int nn = 0, *leaf = nullptr, ln = 0;
-        int rc = pt_bvh_build_ex(b->triangles.data() + b->mesh_start[m], b->mesh_count[m], b->mesh_start[m], leaf_size,
-                                 method, bucket_num, &nodes, &nn, &leaf, &ln);
+        // MortonCodeCUDA runs on the GPU (pt_bvh.hip); its node array equals the host builder's bit for bit
+        // (tests/test_bvh_device.py), which therefore serves machines without a HIP device
+        const bool on_device = method == PT_BVH_MORTON_CODE_CUDA &&
+                               (b->bvh_device >= 0 || (b->bvh_device == -2 && pt_device_count() > 0));
+        int rc = on_device ? pt_bvh_build_device(b->triangles.data() + b->mesh_start[m], b->mesh_count[m],
+                                                 b->mesh_start[m], leaf_size, &nodes, &nn, &leaf, &ln)
+                           : pt_bvh_build_ex(b->triangles.data() + b->mesh_start[m], b->mesh_count[m], b->mesh_start[m],
+                                             leaf_size, method, bucket_num, &nodes, &nn, &leaf, &ln);
         if (rc != 0) return rc;
         b->bvh_nodes.push_back(nodes);
         b->bvh_leaf.push_back(leaf);
