@@ -149,6 +149,170 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
     }
 }
 
+// ---- pass_kernel_u: the same pass with walks and shading interleaved per lane -------------------
+// pass_kernel runs one whole trace step (spheres, every mesh walk, shading) per loop iteration for
+// all lanes together, so a wave walks as long as its longest walk while finished lanes idle. Here a
+// lane is a small state machine: WALK (one BVH node per step of the mesh in flight, then the next
+// mesh), READY (closest hit known) and, for the wave, a SHADE step that runs shade_hit for every
+// READY lane at once — taken when no lane is walking or at least shade_min lanes are ready — after
+// which a surviving path starts its next segment (spheres, mesh 0) and an ended one takes a new
+// pixel. Every lane still computes exactly the reference sequence for its path (same node order,
+// same tests, same draws keyed by (pass, pixel, depth)); only the interleaving between lanes changes.
+enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3 };
+
+// Starts the walk of the first mesh at or after `mesh` with a non-empty node range.
+__device__ __forceinline__ bool start_mesh(const DevScene& sc, int& mesh, MeshWalk& w) {
+    const int2* mr = uniform_ptr(sc.mesh_range);
+    while (mesh < sc.mesh_num) {
+        const int2 r = mr[mesh];
+        if (r.x != r.y) {
+            w.pos = r.x; w.end = r.y;
+            w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
+            return true;
+        }
+        mesh++;
+    }
+    return false;
+}
+
+// Start of one trace_ray_kernel invocation (path_tracer_kernel.cu:418-454): brute-force spheres into
+// the closest hit, then the walk of mesh 0.
+__device__ __forceinline__ int begin_segment(const DevScene& sc, const PathState& ps, v3& inv, Hit& h, MeshWalk& w,
+                                             int& mesh) {
+    h.t = __builtin_inff(); h.t1 = __builtin_inff(); h.t2 = __builtin_inff();
+    h.type = 0; h.prim = -1;
+    for (int i = 0; i < sc.sphere_num; i++) {
+        float t;
+        if (sphere_t(sc.spheres[2 * i], ps.o, ps.d, &t) && t < h.t && t > 0.0f) {
+            h.t = t; h.prim = i; h.type = 1;
+        }
+    }
+    mesh = 0;
+    if (sc.mesh_num > 0) inv = 1.0f / ps.d;
+    return start_mesh(sc, mesh, w) ? LANE_WALK : LANE_READY;
+}
+
+// pixel_256_transform_gamma_corrected_kernel (:644-680) for one finished (pixel, pass) unit
+__device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfig& cfg, const DevOutput& out,
+                                            const PathState& ps, unsigned int unit, int first_pass, int write_u8,
+                                            int batch_log2, float clamp_hi) {
+    const v3 c = clamp3(ps.rad, 0.0f, clamp_hi);
+    if (batch_log2 == 0) {
+        const int pixel = unit_to_pixel(til, unit);
+        float* img = out.image + (size_t)pixel * 3;
+        v3 sum;
+        if (first_pass != 1) sum = mk3(img[0], img[1], img[2]) + c;
+        else sum = c;
+        img[0] = sum.x; img[1] = sum.y; img[2] = sum.z;
+        if (write_u8 && out.image256) store_u8(cfg, sum, first_pass, out.image256 + (size_t)pixel * 3);
+    } else {
+        float* pr = out.pass_rad + (size_t)unit * 3;
+        pr[0] = c.x; pr[1] = c.y; pr[2] = c.z;
+    }
+}
+
+template <int MINW>
+__global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
+                                                                int write_u8, int chunk, int batch_log2, int shade_min,
+                                                                int walk_steps) {
+    const int lane = threadIdx.x & 63;
+    const LaunchParams* P0 = params;
+    const float clamp_hi = (float)P0->cfg.max_depth * 2.0f;
+    const unsigned long long lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+    PathState ps;
+    v3 inv = mk3(0.0f, 0.0f, 0.0f);
+    Hit h;
+    MeshWalk w;
+    int mesh = 0;
+    unsigned int unit = 0;
+    int32_t pseed = 0;
+    int depth = 0;
+    int mode = LANE_WANT;
+    unsigned long long segments = 0;
+    Counters none = {0u, 0u, 0u, 0u, 0u, 0u};
+    const unsigned int units = (unsigned int)P0->til.unit_count << batch_log2;
+    const EvenRegions regions{units, (units + PT_SHARDS - 1) / PT_SHARDS};
+    WorkCursor cursor = work_begin();
+    bool drained = false;
+
+    while (true) {
+        const LaunchParams* P = params;
+        asm volatile("" : "+s"(P));
+        P = uniform_ptr(P);
+        const DevScene sc = load_const(&P->sc);
+        const DevConfig cfg = load_const(&P->cfg);
+        const DevTiling til = load_const(&P->til);
+        const DevOutput out = load_const(&P->out);
+
+        // lanes without a path take the next (pixel, pass) units, one atomic per wave (pt_work.h)
+        const bool want = mode == LANE_WANT;
+        const unsigned long long need_mask = __ballot(want);
+        if (need_mask) {
+            const unsigned int u = work_take(out.fetch, regions.stride, regions, (unsigned int)chunk, need_mask, want,
+                                             lane_lt, cursor, drained);
+            if (want) {
+                if (u != ~0u) {
+                    unit = u;
+                    const int pixel = unit_to_pixel(til, u >> batch_log2);
+                    const int32_t hseed = hash_pt(first_pass + (int)(u & ((1u << batch_log2) - 1u)));
+                    const DevCamera cam = load_const(&P->cam);
+                    generate_path(cam, cfg, pixel, hseed, &ps);
+                    pseed = path_seed(hseed, pixel);
+                    depth = 0;
+                    if (cfg.max_depth > 0) {
+                        mode = begin_segment(sc, ps, inv, h, w, mesh);
+                    } else {
+                        finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
+                    }
+                } else if (drained) {
+                    mode = LANE_DONE;
+                }
+            }
+        }
+        if (!__any(mode != LANE_DONE)) break;
+
+        const unsigned long long ready = __ballot(mode == LANE_READY);
+        const unsigned long long walking = __ballot(mode == LANE_WALK);
+        if (ready && (!walking || __popcll(ready) >= (unsigned int)shade_min)) {
+            if (mode == LANE_READY) {
+                // the rest of trace_ray_kernel for this segment (:456-624)
+                const bool alive = shade_hit<false>(sc, cfg, depth, pseed, &ps, h, &none);
+                depth++;
+                segments++;
+                if (!alive || depth >= cfg.max_depth) {
+                    finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
+                    mode = LANE_WANT;
+                } else {
+                    mode = begin_segment(sc, ps, inv, h, w, mesh);
+                }
+            }
+            continue;
+        }
+
+        const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
+        const __amdgpu_buffer_rsrc_t rt = make_rsrc(sc.tri_geom, sc.tri_count * 48);
+        for (int k = 0; k < walk_steps; k++) {
+            if (k > 0 && !__any(mode == LANE_WALK)) break;
+            if (mode == LANE_WALK) {
+                walk_node(rn, rt, ps.o, ps.d, inv, w);
+                if (w.pos == w.end) {
+                    // closest_hit's merge of this mesh's result (:443-454)
+                    if (w.tri >= 0 && w.t < h.t) {
+                        h.t = w.t; h.t1 = w.t1; h.t2 = w.t2; h.prim = w.tri; h.type = 2;
+                    }
+                    mesh++;
+                    mode = start_mesh(sc, mesh, w) ? LANE_WALK : LANE_READY;
+                }
+            }
+        }
+    }
+
+    unsigned long long s = segments;
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) atomicAdd(&P0->out.stats[0], s);
+}
+
 // The running sum over a batch of passes, in pass order (path_tracer_kernel.cu:644-651 applied
 // pass after pass), then the 8-bit output of the batch's last pass.
 __global__ __launch_bounds__(PT_BLOCK) void accumulate_kernel(const LaunchParams* __restrict__ P, int first_pass,
@@ -290,18 +454,50 @@ static PassFn pass_fn(bool leaf1, bool stats, int minw, bool qn) {
     return pass_kernel<false, true, 5, false>;
 }
 
-int pass_min_waves() {
+// PT_MIN_WAVES overrides the occupancy target: 8 waves/SIMD for pass_kernel (64 VGPRs), 5 for
+// pass_kernel_u (96 VGPRs, no spills), the measured optimum of each.
+int pass_min_waves(bool unified) {
     static int w = [] {
         const char* e = getenv("PT_MIN_WAVES");
-        int v = e ? atoi(e) : 8;
-        return (v >= 4 && v <= 8) ? v : 8;
+        int v = e ? atoi(e) : 0;
+        return (v >= 4 && v <= 8) ? v : 0;
     }();
-    return w;
+    return w ? w : (unified ? 5 : 8);
 }
+
+// PT_UNIFIED=0 selects pass_kernel for the default configuration (leaf size 1, uninstrumented, exact
+// nodes); otherwise pass_kernel_u runs it. PT_SHADE_MIN / PT_WALK_STEPS tune pass_kernel_u.
+bool unified_enabled() {
+    static const int on = env_int("PT_UNIFIED", 1, 0, 1);
+    return on != 0;
+}
+
+using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int);
+
+static PassFnU pass_fn_u(int minw) {
+    if (minw == 6) return pass_kernel_u<6>;
+    if (minw == 7) return pass_kernel_u<7>;
+    if (minw == 8) return pass_kernel_u<8>;
+    return pass_kernel_u<5>;
+}
+
+static bool use_unified(bool leaf1, bool stats, bool qn) { return leaf1 && !stats && !qn && unified_enabled(); }
 
 hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int first_pass, int batch_log2,
                        int write_u8, int grid, bool stats, hipStream_t stream) {
-    PassFn fn = pass_fn(leaf1, stats, pass_min_waves(), qn);
+    if (use_unified(leaf1, stats, qn)) {
+        static const int chunk = env_int("PT_CHUNK_MEGA", 0, 0, 4096);
+        static const int shade_min = env_int("PT_SHADE_MIN", 40, 1, 64);
+        static const int walk_steps = env_int("PT_WALK_STEPS", 8, 1, 64);
+        const LaunchParams* a0 = params_dev;
+        int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps;
+        void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6};
+        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true)), dim3(grid), dim3(PT_BLOCK), args, 0,
+                                       stream);
+        if (e != hipSuccess) return e;
+        return hipGetLastError();
+    }
+    PassFn fn = pass_fn(leaf1, stats, pass_min_waves(false), qn);
     const LaunchParams* a0 = params_dev;
     static const int chunk = env_int("PT_CHUNK_MEGA", 0, 0, 4096);
     int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2;
@@ -331,7 +527,8 @@ int pass_grid_size(bool leaf1, bool stats, bool qn) {
     int dev = 0, cus = 0, blocks = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* fn = (const void*)pass_fn(leaf1, stats, pass_min_waves(), qn);
+    const void* fn = use_unified(leaf1, stats, qn) ? (const void*)pass_fn_u(pass_min_waves(true))
+                                                   : (const void*)pass_fn(leaf1, stats, pass_min_waves(false), qn);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, PT_BLOCK, 0) != hipSuccess || blocks <= 0) blocks = 4;
     if (cus <= 0) cus = 256;
     return cus * blocks;

@@ -382,6 +382,34 @@ __device__ __forceinline__ bool mesh_closest_q(const DevScene& sc, int mesh, int
     return hit;
 }
 
+// The walk of mesh_closest one node at a time, for kernels that interleave walks with shading
+// (pass_kernel_u): the state of one in-flight walk over one mesh, leaf size 1. Same node sequence,
+// same tests, same acceptance rule as mesh_closest<true, false>.
+struct MeshWalk {
+    int pos, end;    // current node, end of the mesh's node range
+    float t, t1, t2; // mesh-local closest hit (reference: the local min_t of intersect_triangle_mesh_bvh)
+    int tri;         // -1 = no hit yet
+};
+
+__device__ __forceinline__ void walk_node(const __amdgpu_buffer_rsrc_t rn, const __amdgpu_buffer_rsrc_t rt, v3 o, v3 d,
+                                          v3 inv, MeshWalk& w) {
+    const float4 lo = bload(rn, w.pos * 32), hi = bload(rn, w.pos * 32 + 16);
+    float entry;
+    if (box_hit(lo, hi, o, inv, &entry) && entry <= w.t) {
+        const int slot = f2i(hi.w);
+        if (slot >= 0) {
+            float t, t1, t2;
+            const float4 a = bload(rt, slot * 48), b = bload(rt, slot * 48 + 16), c = bload(rt, slot * 48 + 32);
+            if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t) {
+                w.t = t; w.t1 = t1; w.t2 = t2; w.tri = slot;
+            }
+        }
+        w.pos++;
+    } else {
+        w.pos = f2i(lo.w);
+    }
+}
+
 // Per-path registers (the reference keeps these per pixel in HBM: rays, not_absorbed_colors,
 // accumulated_colors, scatterings; path_tracer_kernel.cu:275-297). The scattering coefficients are
 // always either the configuration's air values or some material's medium (they are only ever copied
