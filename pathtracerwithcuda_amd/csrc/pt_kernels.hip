@@ -158,7 +158,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
 // which a surviving path starts its next segment (spheres, mesh 0) and an ended one takes a new
 // pixel. Every lane still computes exactly the reference sequence for its path (same node order,
 // same tests, same draws keyed by (pass, pixel, depth)); only the interleaving between lanes changes.
-enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3 };
+enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3, LANE_TRI = 4 };
 
 // Starts the walk of the first mesh at or after `mesh` with a non-empty node range.
 __device__ __forceinline__ bool start_mesh(const DevScene& sc, int& mesh, MeshWalk& w) {
@@ -211,10 +211,13 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
     }
 }
 
-template <int MINW>
+// PROF: wave-level occupancy counters of the state machine into stats[16..23] (tools/uprof.py):
+// rounds, walk steps, walking lanes summed over steps, shading batches, lanes shaded, triangle
+// batches, lanes in triangle batches, lanes refilled.
+template <int MINW, bool PROF, bool QN>
 __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
-                                                                int walk_steps) {
+                                                                int walk_steps, int tri_min, int walk_min) {
     const int lane = threadIdx.x & 63;
     const LaunchParams* P0 = params;
     const float clamp_hi = (float)P0->cfg.max_depth * 2.0f;
@@ -225,6 +228,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
     Hit h;
     MeshWalk w;
     int mesh = 0;
+    int ptri = -1;  // leaf triangle awaiting its test (LANE_TRI)
     unsigned int unit = 0;
     int32_t pseed = 0;
     int depth = 0;
@@ -235,6 +239,8 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
     const EvenRegions regions{units, (units + PT_SHARDS - 1) / PT_SHARDS};
     WorkCursor cursor = work_begin();
     bool drained = false;
+    unsigned long long prof[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tc = 0;
 
     while (true) {
         const LaunchParams* P = params;
@@ -244,6 +250,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
         const DevConfig cfg = load_const(&P->cfg);
         const DevTiling til = load_const(&P->til);
         const DevOutput out = load_const(&P->out);
+        if (PROF) { prof[0]++; tc = __builtin_readcyclecounter(); }
 
         // lanes without a path take the next (pixel, pass) units, one atomic per wave (pt_work.h)
         const bool want = mode == LANE_WANT;
@@ -251,6 +258,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
         if (need_mask) {
             const unsigned int u = work_take(out.fetch, regions.stride, regions, (unsigned int)chunk, need_mask, want,
                                              lane_lt, cursor, drained);
+            if (PROF) prof[7] += (unsigned long long)__popcll(__ballot(want && u != ~0u));
             if (want) {
                 if (u != ~0u) {
                     unit = u;
@@ -271,10 +279,12 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
             }
         }
         if (!__any(mode != LANE_DONE)) break;
+        if (PROF) { const unsigned long long t = __builtin_readcyclecounter(); prof[8] += t - tc; tc = t; }
 
         const unsigned long long ready = __ballot(mode == LANE_READY);
-        const unsigned long long walking = __ballot(mode == LANE_WALK);
-        if (ready && (!walking || __popcll(ready) >= (unsigned int)shade_min)) {
+        const unsigned long long walking = __ballot(mode == LANE_WALK || mode == LANE_TRI);
+        if (ready && (__popcll(walking) <= (unsigned int)walk_min || __popcll(ready) >= (unsigned int)shade_min)) {
+            if (PROF) { prof[3]++; prof[4] += (unsigned long long)__popcll(ready); }
             if (mode == LANE_READY) {
                 // the rest of trace_ray_kernel for this segment (:456-624)
                 const bool alive = shade_hit<false>(sc, cfg, depth, pseed, &ps, h, &none);
@@ -287,30 +297,60 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                     mode = begin_segment(sc, ps, inv, h, w, mesh);
                 }
             }
+            if (PROF) prof[9] += __builtin_readcyclecounter() - tc;
             continue;
         }
 
         const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
         const __amdgpu_buffer_rsrc_t rt = make_rsrc(sc.tri_geom, sc.tri_count * 48);
+        __amdgpu_buffer_rsrc_t rq = rn;
+        float4 fb = make_float4(0.0f, 0.0f, 0.0f, 0.0f), fs = fb;
+        if (QN) {
+            rq = make_rsrc(sc.qnodes, sc.node_count * 16);
+            fb = load_const(sc.mesh_q);
+            fs = load_const(sc.mesh_q + 1);
+        }
+        // closest_hit's merge of a finished mesh walk (:443-454), then the next mesh or READY
+        auto mesh_done = [&]() {
+            if (w.tri >= 0 && w.t < h.t) {
+                h.t = w.t; h.t1 = w.t1; h.t2 = w.t2; h.prim = w.tri; h.type = 2;
+            }
+            mesh++;
+            mode = start_mesh(sc, mesh, w) ? LANE_WALK : LANE_READY;
+        };
         for (int k = 0; k < walk_steps; k++) {
-            if (k > 0 && !__any(mode == LANE_WALK)) break;
+            if (k > 0 && !__any(mode == LANE_WALK || mode == LANE_TRI)) break;
+            if (PROF) { prof[1]++; prof[2] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK)); }
             if (mode == LANE_WALK) {
-                walk_node(rn, rt, ps.o, ps.d, inv, w);
-                if (w.pos == w.end) {
-                    // closest_hit's merge of this mesh's result (:443-454)
-                    if (w.tri >= 0 && w.t < h.t) {
-                        h.t = w.t; h.t1 = w.t1; h.t2 = w.t2; h.prim = w.tri; h.type = 2;
-                    }
-                    mesh++;
-                    mode = start_mesh(sc, mesh, w) ? LANE_WALK : LANE_READY;
+                const bool leaf = QN ? walk_box_q(rq, fb, fs, ps.o, inv, w, ptri) : walk_box(rn, ps.o, inv, w, ptri);
+                if (leaf) mode = LANE_TRI;
+                else if (w.pos == w.end) mesh_done();
+            }
+            // leaf triangles are tested in batches of at least tri_min lanes (or when no lane can
+            // walk on): the triangle test then runs with many lanes active instead of one or two
+            const unsigned long long pend = __ballot(mode == LANE_TRI);
+            if (pend && (__popcll(pend) >= (unsigned int)tri_min || !__any(mode == LANE_WALK))) {
+                if (PROF) { prof[5]++; prof[6] += (unsigned long long)__popcll(pend); }
+                if (mode == LANE_TRI) {
+                    if (QN) walk_tri_q(rn, rt, ps.o, ps.d, inv, w, ptri);
+                    else walk_tri(rt, ps.o, ps.d, w, ptri);
+                    mode = LANE_WALK;
+                    if (w.pos == w.end) mesh_done();
                 }
             }
         }
+        if (PROF) prof[10] += __builtin_readcyclecounter() - tc;
     }
 
     unsigned long long s = segments;
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0) atomicAdd(&P0->out.stats[0], s);
+    if (lane == 0) {
+        atomicAdd(&P0->out.stats[0], s);
+        if (PROF) {
+#pragma unroll
+            for (int k = 0; k < 11; k++) atomicAdd(&P0->out.stats[16 + k], prof[k]);
+        }
+    }
 }
 
 // The running sum over a batch of passes, in pass order (path_tracer_kernel.cu:644-651 applied
@@ -472,16 +512,19 @@ bool unified_enabled() {
     return on != 0;
 }
 
-using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int);
+using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int, int);
 
-static PassFnU pass_fn_u(int minw) {
-    if (minw == 6) return pass_kernel_u<6>;
-    if (minw == 7) return pass_kernel_u<7>;
-    if (minw == 8) return pass_kernel_u<8>;
-    return pass_kernel_u<5>;
+static PassFnU pass_fn_u(int minw, bool qn) {
+    static const int prof = env_int("PT_UPROF", 0, 0, 1);
+    if (prof) return qn ? pass_kernel_u<5, true, true> : pass_kernel_u<5, true, false>;
+    if (qn) return minw == 6 ? pass_kernel_u<6, false, true> : pass_kernel_u<5, false, true>;
+    if (minw == 6) return pass_kernel_u<6, false, false>;
+    if (minw == 7) return pass_kernel_u<7, false, false>;
+    if (minw == 8) return pass_kernel_u<8, false, false>;
+    return pass_kernel_u<5, false, false>;
 }
 
-static bool use_unified(bool leaf1, bool stats, bool qn) { return leaf1 && !stats && !qn && unified_enabled(); }
+static bool use_unified(bool leaf1, bool stats, bool qn) { (void)qn; return leaf1 && !stats && unified_enabled(); }
 
 hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int first_pass, int batch_log2,
                        int write_u8, int grid, bool stats, hipStream_t stream) {
@@ -490,9 +533,12 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int 
         static const int shade_min = env_int("PT_SHADE_MIN", 40, 1, 64);
         static const int walk_steps = env_int("PT_WALK_STEPS", 8, 1, 64);
         const LaunchParams* a0 = params_dev;
-        int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps;
-        void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6};
-        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true)), dim3(grid), dim3(PT_BLOCK), args, 0,
+        static const int tri_min = env_int("PT_TRI_MIN", 4, 1, 64);
+        static const int walk_min = env_int("PT_WALK_MIN", 8, 0, 64);
+        int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
+            a8 = walk_min;
+        void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8};
+        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn), dim3(grid), dim3(PT_BLOCK), args, 0,
                                        stream);
         if (e != hipSuccess) return e;
         return hipGetLastError();
@@ -527,7 +573,7 @@ int pass_grid_size(bool leaf1, bool stats, bool qn) {
     int dev = 0, cus = 0, blocks = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* fn = use_unified(leaf1, stats, qn) ? (const void*)pass_fn_u(pass_min_waves(true))
+    const void* fn = use_unified(leaf1, stats, qn) ? (const void*)pass_fn_u(pass_min_waves(true), qn)
                                                    : (const void*)pass_fn(leaf1, stats, pass_min_waves(false), qn);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, PT_BLOCK, 0) != hipSuccess || blocks <= 0) blocks = 4;
     if (cus <= 0) cus = 256;

@@ -410,6 +410,76 @@ __device__ __forceinline__ void walk_node(const __amdgpu_buffer_rsrc_t rn, const
     }
 }
 
+// walk_node split at the leaf: the box stage (returns true with the leaf's triangle when the leaf box
+// passes, without advancing) and the triangle stage (tests it, then advances). A lane runs them
+// back to back; between them it may wait while other lanes catch up (pass_kernel_u batches the
+// triangle stage), which changes nothing in its own sequence of tests.
+__device__ __forceinline__ bool walk_box(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri) {
+    const float4 lo = bload(rn, w.pos * 32), hi = bload(rn, w.pos * 32 + 16);
+    float entry;
+    if (box_hit(lo, hi, o, inv, &entry) && entry <= w.t) {
+        const int slot = f2i(hi.w);
+        if (slot >= 0) {
+            tri = slot;
+            return true;
+        }
+        w.pos++;
+    } else {
+        w.pos = f2i(lo.w);
+    }
+    return false;
+}
+
+__device__ __forceinline__ void walk_tri(const __amdgpu_buffer_rsrc_t rt, v3 o, v3 d, MeshWalk& w, int tri) {
+    float t, t1, t2;
+    const float4 a = bload(rt, tri * 48), b = bload(rt, tri * 48 + 16), c = bload(rt, tri * 48 + 32);
+    if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t) {
+        w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
+    }
+    w.pos++;
+}
+
+// The same two stages on the 16-B quantised nodes (mesh_closest_q's rules) with the scene-wide frame
+// (fb, fs, wave-uniform): the box stage tests the outward-rounded box; a leaf's triangle then counts
+// only if the reference's own exact leaf test passes too, which walk_tri_q checks with the exact
+// 32-B node loaded alongside the triangle (no extra dependent round trip).
+__device__ __forceinline__ bool walk_box_q(const __amdgpu_buffer_rsrc_t rq, float4 fb, float4 fs, v3 o, v3 inv,
+                                           MeshWalk& w, int& tri) {
+    const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rq, w.pos * 16, 0, 0);
+    float4 lo, hi;
+    lo.x = fb.x + (float)(q.x & 0xffffu) * fs.x;
+    lo.y = fb.y + (float)(q.x >> 16) * fs.y;
+    lo.z = fb.z + (float)(q.y & 0xffffu) * fs.z;
+    hi.x = fb.x + (float)(q.y >> 16) * fs.x;
+    hi.y = fb.y + (float)(q.z & 0xffffu) * fs.y;
+    hi.z = fb.z + (float)(q.z >> 16) * fs.z;
+    const int link = (int)q.w;
+    float entry;
+    if (box_hit(lo, hi, o, inv, &entry) && entry <= w.t) {
+        if (link < 0) {
+            tri = link & 0x7fffffff;
+            return true;
+        }
+        w.pos++;
+    } else {
+        w.pos = link < 0 ? w.pos + 1 : link;
+    }
+    return false;
+}
+
+__device__ __forceinline__ void walk_tri_q(const __amdgpu_buffer_rsrc_t rn, const __amdgpu_buffer_rsrc_t rt, v3 o, v3 d,
+                                           v3 inv, MeshWalk& w, int tri) {
+    float t, t1, t2;
+    const float4 lo = bload(rn, w.pos * 32), hi = bload(rn, w.pos * 32 + 16);
+    const float4 a = bload(rt, tri * 48), b = bload(rt, tri * 48 + 16), c = bload(rt, tri * 48 + 32);
+    float ee;
+    if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t && box_hit(lo, hi, o, inv, &ee) &&
+        ee <= w.t) {
+        w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
+    }
+    w.pos++;
+}
+
 // Per-path registers (the reference keeps these per pixel in HBM: rays, not_absorbed_colors,
 // accumulated_colors, scatterings; path_tracer_kernel.cu:275-297). The scattering coefficients are
 // always either the configuration's air values or some material's medium (they are only ever copied

@@ -117,25 +117,26 @@ void quantise_nodes(SceneStage& st) {
     st.mesh_q.clear();
     if (st.leaf_size != 1) return;
     std::vector<uint4> q(st.nodes.size() / 2);
-    for (const int2& r : st.mesh_range) {
-        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        for (int i = r.x; i < r.y; i++) {
-            const float4& a = st.nodes[2 * i];
-            const float4& b = st.nodes[2 * i + 1];
-            const float l[3] = {a.x, a.y, a.z}, h[3] = {b.x, b.y, b.z};
-            for (int k = 0; k < 3; k++) {
-                if (!std::isfinite(l[k]) || !std::isfinite(h[k])) return;
-                lo[k] = std::min(lo[k], l[k]);
-                hi[k] = std::max(hi[k], h[k]);
-            }
-        }
-        float step[3] = {0.0f, 0.0f, 0.0f};
+    // one frame for the whole scene (every mesh_q entry equal), so a walk can hold it in SGPRs
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (size_t i = 0; i < st.nodes.size() / 2; i++) {
+        const float4& a = st.nodes[2 * i];
+        const float4& b = st.nodes[2 * i + 1];
+        const float l[3] = {a.x, a.y, a.z}, h[3] = {b.x, b.y, b.z};
         for (int k = 0; k < 3; k++) {
-            if (r.x == r.y || hi[k] <= lo[k]) continue;
-            step[k] = (float)(((double)hi[k] - (double)lo[k]) / 65534.0);
-            if (!(step[k] > 0.0f)) step[k] = std::numeric_limits<float>::denorm_min();
-            while (dequant(lo[k], step[k], 65535u) < hi[k]) step[k] = std::nextafter(step[k], INFINITY);
+            if (!std::isfinite(l[k]) || !std::isfinite(h[k])) return;
+            lo[k] = std::min(lo[k], l[k]);
+            hi[k] = std::max(hi[k], h[k]);
         }
+    }
+    float step[3] = {0.0f, 0.0f, 0.0f};
+    for (int k = 0; k < 3; k++) {
+        if (st.nodes.empty() || hi[k] <= lo[k]) continue;
+        step[k] = (float)(((double)hi[k] - (double)lo[k]) / 65534.0);
+        if (!(step[k] > 0.0f)) step[k] = std::numeric_limits<float>::denorm_min();
+        while (dequant(lo[k], step[k], 65535u) < hi[k]) step[k] = std::nextafter(step[k], INFINITY);
+    }
+    for (const int2& r : st.mesh_range) {
         st.mesh_q.push_back(mkf4(lo[0], lo[1], lo[2], 0.0f));
         st.mesh_q.push_back(mkf4(step[0], step[1], step[2], 0.0f));
         for (int i = r.x; i < r.y; i++) {

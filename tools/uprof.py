@@ -1,0 +1,40 @@
+"""State-machine occupancy of pass_kernel_u on the benchmark frame (PT_UPROF=1 build of the kernel):
+rounds, walk steps and walking lanes per step, shading / triangle batches and their lanes."""
+import ctypes as C
+import json
+import os
+import sys
+
+os.environ["PT_UPROF"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+import pathtracerwithcuda_amd as pt  # noqa: E402
+
+r = pt.Renderer(0)
+scene = pt.cornell_scene(pt.torus_knot(*bench.KNOT))
+cfg = pt.configuration(max_tracer_depth=bench.DEPTH)
+cam = pt.camera(bench.WIDTH, bench.HEIGHT, **bench.CAMERA)
+r.upload(scene, cfg)
+r.setup_frame(bench.WIDTH, bench.HEIGHT)
+r.render(cam, cfg, 1, bench.SPP, write_u8=2)
+r.synchronize()
+r.stats_reset()
+r.render(cam, cfg, 1, bench.SPP, write_u8=2)
+r.synchronize()
+buf = (C.c_ulonglong * 32)()
+pt.lib().pt_stats_all(r._ctx, buf, 32)
+v = list(buf)
+names = ["rounds", "walk_steps", "walking_lanes", "shade_batches", "lanes_shaded", "tri_batches", "tri_lanes", "refilled",
+         "cyc_refill", "cyc_shade", "cyc_walk"]
+d = {n: v[16 + i] for i, n in enumerate(names)}
+d["segments"] = v[0]
+d["lanes_per_walk_step"] = round(d["walking_lanes"] / max(d["walk_steps"], 1), 2)
+d["lanes_per_shade_batch"] = round(d["lanes_shaded"] / max(d["shade_batches"], 1), 2)
+d["lanes_per_tri_batch"] = round(d["tri_lanes"] / max(d["tri_batches"], 1), 2)
+d["walk_steps_per_round"] = round(d["walk_steps"] / max(d["rounds"], 1), 2)
+tot = d["cyc_refill"] + d["cyc_shade"] + d["cyc_walk"]
+for k in ("cyc_refill", "cyc_shade", "cyc_walk"):
+    d[k.replace("cyc", "frac")] = round(d[k] / max(tot, 1), 3)
+d["cyc_per_walk_round"] = round(d["cyc_walk"] / max(d["rounds"] - d["shade_batches"], 1))
+d["cyc_per_shade_batch"] = round(d["cyc_shade"] / max(d["shade_batches"], 1))
+print(json.dumps(d))
