@@ -22,6 +22,7 @@ hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256
                      hipStream_t stream);
 int pass_grid_size(bool leaf1, bool stats, bool qn);
 int env_int(const char* name, int dflt, int lo, int hi);  // clamped integer from the environment
+hipError_t launch_material_consts(DevMaterial* mats, int n, float air_n, hipStream_t stream);
 hipError_t launch_math_eval(int which, const float* x, int n, float* o0, float* o1, hipStream_t stream);
 hipError_t shrink(int* data, int n, int* scratch, int* tile_counts, int* total_dev, int* total_host,
                   hipStream_t stream);

@@ -383,6 +383,25 @@ __global__ __launch_bounds__(PT_BLOCK) void u8_kernel(DevConfig cfg, const float
     store_u8(cfg, mk3(p[0], p[1], p[2]), pass, image256 + (size_t)i * 3);
 }
 
+// Per-material constants of shade_hit (DevMaterial::rough_alpha / tir_front / tir_back), with the
+// expressions shade_hit evaluated per hit before: pow(roughness, 1.85) * 0.238 (:571) and
+// asin(out_n / in_n) of the dielectric TIR test (fresnel.h:34) for both sides of the surface.
+__global__ __launch_bounds__(PT_BLOCK) void material_consts_kernel(DevMaterial* mats, int n, float air_n) {
+    const int i = blockIdx.x * PT_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    DevMaterial& m = mats[i];
+    m.rough_alpha = pow_pt(m.roughness, 1.85f) * 0.238f;
+    m.tir_front = asin_pt(m.refraction_index / air_n);
+    m.tir_back = asin_pt(air_n / m.refraction_index);
+}
+
+hipError_t launch_material_consts(DevMaterial* mats, int n, float air_n, hipStream_t stream) {
+    if (n <= 0 || !mats) return hipSuccess;
+    hipLaunchKernelGGL(material_consts_kernel, dim3((n + PT_BLOCK - 1) / PT_BLOCK), dim3(PT_BLOCK), 0, stream, mats, n,
+                       air_n);
+    return hipGetLastError();
+}
+
 // Diagnostic: the device transcendentals on an array (bitwise check against the oracle's).
 __global__ __launch_bounds__(PT_BLOCK) void math_eval_kernel(int which, const float* x, int n, float* o0, float* o1) {
     int i = blockIdx.x * PT_BLOCK + threadIdx.x;

@@ -82,6 +82,17 @@ __device__ __forceinline__ void tangent_frame(v3 n, v3* vi, v3* vj) {
     *vj = cross(n, *vi);
 }
 
+// The common tail of sample_on_hemisphere_cosine_weight / _ggx_weight (path_tracer_kernel.cu:174-191):
+// the tangent frame of n and the direction at (theta, phi = 2 pi r2).
+__device__ __forceinline__ v3 hemisphere_dir(v3 n, float cos_theta, float sin_theta, float r2) {
+    float phi = r2 * kTWO_PI;
+    v3 vi, vj;
+    tangent_frame(n, &vi, &vj);
+    float sp, cp;
+    sincos_pt(phi, &sp, &cp);
+    return cos_theta * n + cp * sin_theta * vi + sp * sin_theta * vj;
+}
+
 // path_tracer_kernel.cu:163-192
 __device__ __forceinline__ v3 sample_cosine(v3 n, float r1, float r2) {
     float cos_theta = sqrtf(r1);
@@ -135,11 +146,12 @@ __device__ __forceinline__ float ggx_g1(float roughness, v3 macro, v3 micro, v3 
     return 2.0f / (1.0f + sqrtf(1.0f + r2 * t2));
 }
 
-// Core/fresnel.h:11-49 (pow(x, 2.0f) -> x*x)
-__device__ __forceinline__ float fresnel_dielectric(v3 n, v3 in, float in_n, float out_n, v3 refr) {
+// Core/fresnel.h:11-49 (pow(x, 2.0f) -> x*x). tir_asin = asin(out_n / in_n), precomputed per material
+// (DevMaterial::tir_front / tir_back; only read when in_n > out_n).
+__device__ __forceinline__ float fresnel_dielectric(v3 n, v3 in, float in_n, float out_n, v3 refr, float tir_asin) {
     float cos_in = dot(n, in * -1.0f);
     float cos_out = dot(-1.0f * n, refr);
-    if (in_n > out_n && acos_pt(cos_in) >= asin_pt(out_n / in_n)) return 1.0f;
+    if (in_n > out_n && acos_pt(cos_in) >= tir_asin) return 1.0f;
     if (length(refr) <= 0.000005f || cos_out < 0) return 1.0f;
     float s = (in_n * cos_in - out_n * cos_out) / (in_n * cos_in + out_n * cos_out);
     float p = (in_n * cos_out - out_n * cos_in) / (in_n * cos_out + out_n * cos_in);
@@ -678,37 +690,49 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
 
     float R;
     const float k = M.extinction_coefficient;
-    if (k == 0 || transparent) R = fresnel_dielectric(normal, d, in_n, out_n, refr);
+    if (k == 0 || transparent) R = fresnel_dielectric(normal, d, in_n, out_n, refr, out_medium < 0 ? M.tir_back : M.tir_front);
     else R = fresnel_conductor(normal, d, out_n, k);
 
+    // Bounce (:563-610). The reflect and diffuse branches both draw r1, r2 right after r and build
+    // their direction with the same hemisphere tail, so the draws and the tail are shared (a refract
+    // lane draws them too and ignores them: the generator is local to this step).
     float r = minstd_uniform(&rng, 0.0f, 1.0f);
-    if (r < R) {  // reflection (:565-584)
-        float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
-        float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
-        float rough = pow_pt(M.roughness, 1.85f) * 0.238f;
-        v3 micro = sample_ggx(normal, rough, r1, r2);
-        v3 mr = reflection(micro, d);
-        float shadow = ggx_g1(rough, normal, micro, d) * ggx_g1(rough, normal, micro, mr);
-        v3 spec = mk3(M.specular[0], M.specular[1], M.specular[2]);
-        if (has_tex_s) spec = spec * tex_s;
-        ps->o = point + bias_v;
-        ps->d = mr;
-        ps->thr = ps->thr * (spec * shadow);
-    } else if (transparent) {  // refraction (:585-596)
+    const bool reflect = r < R;
+    float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
+    float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
+    if (reflect || !transparent) {
+        float cos_t, sin_t;
+        if (reflect) {  // sample_on_hemisphere_ggx_weight (:194-223), alpha = roughness^1.85 * 0.238 (:571)
+            const float theta = atan_pt(M.rough_alpha * sqrtf(r1) / sqrtf(1.0f - r1));
+            sincos_pt(theta, &sin_t, &cos_t);
+        } else {        // sample_on_hemisphere_cosine_weight (:163-192)
+            cos_t = sqrtf(r1);
+            sin_t = sqrtf(1.0f - cos_t * cos_t);
+        }
+        const v3 dir = hemisphere_dir(normal, cos_t, sin_t, r2);
+        if (reflect) {  // reflection (:565-584)
+            const float rough = M.rough_alpha;
+            v3 mr = reflection(dir, d);
+            float shadow = ggx_g1(rough, normal, dir, d) * ggx_g1(rough, normal, dir, mr);
+            v3 spec = mk3(M.specular[0], M.specular[1], M.specular[2]);
+            if (has_tex_s) spec = spec * tex_s;
+            ps->o = point + bias_v;
+            ps->d = mr;
+            ps->thr = ps->thr * (spec * shadow);
+        } else {        // diffuse (:597-610)
+            v3 diff = mk3(M.diffuse[0], M.diffuse[1], M.diffuse[2]);
+            if (has_tex_d) diff = diff * tex_d;
+            ps->rad = ps->rad + ps->thr * mk3(M.emission[0], M.emission[1], M.emission[2]);
+            ps->thr = ps->thr * diff;
+            ps->o = point + bias_v;
+            ps->d = dir;
+        }
+    } else {  // refraction (:585-596)
         ps->o = point - bias_v;
         ps->d = refr;
         ps->medium = out_medium;
         float ratio = out_n / in_n;
         ps->thr = ps->thr * (ratio * ratio);
-    } else {  // diffuse (:597-610)
-        v3 diff = mk3(M.diffuse[0], M.diffuse[1], M.diffuse[2]);
-        if (has_tex_d) diff = diff * tex_d;
-        ps->rad = ps->rad + ps->thr * mk3(M.emission[0], M.emission[1], M.emission[2]);
-        ps->thr = ps->thr * diff;
-        float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
-        float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
-        ps->o = point + bias_v;
-        ps->d = sample_cosine(normal, r1, r2);
     }
     return length(ps->thr) > cfg.energy_threshold;
 }

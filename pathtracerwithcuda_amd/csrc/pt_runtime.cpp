@@ -311,6 +311,9 @@ struct pt_context {
     DevScene scene{};
     int node_num = 0, tri_num = 0;
     bool has_scene = false;
+    int material_num = 0;
+    float mat_air_n = 0.0f;       // air index the per-material constants were computed for
+    bool mat_air_n_valid = false;
     // frame
     int width = 0, height = 0;
     float* image = nullptr;        // float3
@@ -413,6 +416,8 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     s.tri_count = (int)(st.tri_geom.size() / 3);
     ctx->node_num = (int)(st.nodes.size() / 2);
     ctx->tri_num = (int)(st.tri_geom.size() / 3);
+    ctx->material_num = (int)st.mats.size();
+    ctx->mat_air_n_valid = false;
     ctx->has_scene = true;
     return PT_OK;
 }
@@ -581,6 +586,12 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     lp.til = ctx->tiling;
     lp.out = out;
     const int D = dc.max_depth > 0 ? dc.max_depth : 0;
+    if (!ctx->mat_air_n_valid || ctx->mat_air_n != dc.air_n) {  // DevMaterial shading constants
+        PT_HIP(launch_material_consts(const_cast<DevMaterial*>(ctx->scene.materials), ctx->material_num, dc.air_n,
+                                      ctx->stream));
+        ctx->mat_air_n = dc.air_n;
+        ctx->mat_air_n_valid = true;
+    }
     if (ctx->schedule == PT_SCHEDULE_WAVEFRONT || (ctx->schedule < 0 && use_wavefront())) {
         int rc = ensure_wave(ctx, ctx->tiling.unit_count, D);
         if (rc != PT_OK) return rc;

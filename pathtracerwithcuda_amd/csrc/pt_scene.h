@@ -48,7 +48,11 @@ struct alignas(16) DevMaterial {
     int is_transparent;
     int diffuse_texture_id;
     int specular_texture_id;
-    int pad[3];
+    // per-material constants of the shading math, computed on the device by material_consts_kernel
+    // with the same functions shade_hit would call (so the values are the ones it would compute):
+    float rough_alpha;  // pow(roughness, 1.85) * 0.238 (path_tracer_kernel.cu:571)
+    float tir_front;    // asin(n / air_n): fresnel.h:34 TIR threshold entering the material
+    float tir_back;     // asin(air_n / n): the same leaving it (transparent back face)
 };
 static_assert(sizeof(DevMaterial) == 96, "DevMaterial layout");
 
