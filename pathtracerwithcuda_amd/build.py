@@ -17,6 +17,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(LIBDIR, "libpt_hip.so")
+CLI = os.path.join(LIBDIR, "pt_render")  # headless host program (csrc/pt_cli.cpp) linked against LIB
 
 ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
@@ -52,7 +53,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objdir = os.path.join(LIBDIR, "obj")
     os.makedirs(objdir, exist_ok=True)
     deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE)]
-    if not force and not _sources_newer(LIB, deps):
+    if not force and not _sources_newer(LIB, deps) and not _sources_newer(CLI, deps):
         return LIB
     hipcc = _hipcc()
     jobs = []
@@ -72,6 +73,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
     tmp = LIB + ".tmp"
     _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, *LINK_LIBS, "-o", tmp])
     os.replace(tmp, LIB)
+    _run(["g++", *COMMON, os.path.join(CSRC, "pt_cli.cpp"), "-o", CLI + ".tmp", f"-L{LIBDIR}", "-lpt_hip",
+          "-Wl,-rpath,$ORIGIN"])
+    os.replace(CLI + ".tmp", CLI)
     return LIB
 
 
