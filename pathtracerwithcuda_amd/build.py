@@ -14,7 +14,8 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-LIBDIR = os.path.join(HERE, "lib")
+# PT_LIBDIR / PT_EXTRA_FLAGS: an alternative build (compiler-flag A/B runs); the product is lib/
+LIBDIR = os.environ.get("PT_LIBDIR") or os.path.join(HERE, "lib")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(LIBDIR, "libpt_hip.so")
 CLI = os.path.join(LIBDIR, "pt_render")  # headless host program (csrc/pt_cli.cpp) linked against LIB
@@ -22,6 +23,10 @@ CLI = os.path.join(LIBDIR, "pt_render")  # headless host program (csrc/pt_cli.cp
 ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
           f"-I{INCLUDE}", f"-I{CSRC}"]
+# -fno-slp-vectorize: the SLP pass packs independent fp32 lanes into v_pk_* ops that need extra
+# v_mov shuffles and 3 more VGPRs; without it pass_kernel_u is 3.6% faster (profiles/r01/ab_slp.txt).
+# It does not change a single rounding (no contraction, no reassociation): parity stays bit-exact.
+HIP_FLAGS = ["-fno-slp-vectorize"] + os.environ.get("PT_EXTRA_FLAGS", "").split()
 
 HIP_SOURCES = ["pt_kernels.hip", "pt_wavefront.hip", "pt_bvh.hip", "pt_runtime.cpp"]
 CXX_SOURCES = ["pt_host.cpp", "pt_loader.cpp", "pt_image.cpp"]
@@ -61,7 +66,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for src in HIP_SOURCES:
         obj = os.path.join(objdir, src + ".o")
         objs.append(obj)
-        jobs.append([hipcc, "-x", "hip", f"--offload-arch={ARCH}", *COMMON, "-c", os.path.join(CSRC, src), "-o", obj])
+        jobs.append([hipcc, "-x", "hip", f"--offload-arch={ARCH}", *COMMON, *HIP_FLAGS, "-c", os.path.join(CSRC, src), "-o", obj])
     for src in CXX_SOURCES:
         obj = os.path.join(objdir, src + ".o")
         objs.append(obj)

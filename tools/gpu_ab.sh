@@ -13,7 +13,7 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 for v in "$@"; do
   echo "== $v"
-  f=gpurun_out/$TAG/bench_$(echo $v | tr '= ' '__').json
+  f=gpurun_out/$TAG/bench_$(echo $v | tr '= /' '___').json
   env $v timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > $f 2>/dev/null || exit $?
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], 'Mrays/s', d['ms_per_step'], 'ms/frame', d['roofline']['avg_launch_ms'], 'ms/launch')" $f
 done
