@@ -19,6 +19,22 @@
 
 namespace pt {
 
+// PT_DUP (diagnostic builds only, -DPT_DUP=n via PT_EXTRA_FLAGS into a separate PT_LIBDIR): run one
+// phase twice on opaque copies of its inputs and discard the copy's result, so that the PMC
+// difference SQ_INSTS_VALU(dup) - SQ_INSTS_VALU(normal) is the VALU count of that phase over the
+// same dynamic paths (1 shading, 2 box stage, 3 triangle stage, 4 path generation). The product
+// build has PT_DUP 0 and none of this code.
+#ifndef PT_DUP
+#define PT_DUP 0
+#endif
+template <class T>
+__device__ __forceinline__ void opaque(T& x) {
+    int* p = reinterpret_cast<int*>(&x);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); i++) asm volatile("" : "+v"(p[i]));
+}
+
+
 // A copy of *p read through the constant address space: the loads are known not to alias the
 // kernel's stores, so a wave-uniform p becomes scalar loads into SGPRs (s_load_dwordx*), not
 // vector loads that cost VGPRs and vector-memory issue slots.
@@ -265,6 +281,12 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                     const int pixel = unit_to_pixel(til, u >> batch_log2);
                     const int32_t hseed = hash_pt(first_pass + (int)(u & ((1u << batch_log2) - 1u)));
                     const DevCamera cam = load_const(&P->cam);
+                    if (PT_DUP == 4) {
+                        PathState p2; int px2 = pixel, hs2 = hseed;
+                        opaque(px2); opaque(hs2);
+                        generate_path(cam, cfg, px2, hs2, &p2);
+                        opaque(p2);
+                    }
                     generate_path(cam, cfg, pixel, hseed, &ps);
                     pseed = path_seed(hseed, pixel);
                     depth = 0;
@@ -287,6 +309,12 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
             if (PROF) { prof[3]++; prof[4] += (unsigned long long)__popcll(ready); }
             if (mode == LANE_READY) {
                 // the rest of trace_ray_kernel for this segment (:456-624)
+                if (PT_DUP == 1) {
+                    PathState p2 = ps; Hit h2 = h; int d2 = depth;
+                    opaque(p2); opaque(h2); opaque(d2);
+                    bool a2 = shade_hit<false>(sc, cfg, d2, pseed, &p2, h2, &none);
+                    opaque(p2); opaque(a2);
+                }
                 const bool alive = shade_hit<false>(sc, cfg, depth, pseed, &ps, h, &none);
                 depth++;
                 segments++;
@@ -322,6 +350,12 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
             if (k > 0 && !__any(mode == LANE_WALK || mode == LANE_TRI)) break;
             if (PROF) { prof[1]++; prof[2] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK)); }
             if (mode == LANE_WALK) {
+                if (PT_DUP == 2) {
+                    MeshWalk w2 = w; v3 o2 = ps.o, i2 = inv; int t2 = ptri;
+                    opaque(w2); opaque(o2); opaque(i2);
+                    bool l2 = walk_box(rn, o2, i2, w2, t2);
+                    opaque(w2); opaque(l2); opaque(t2);
+                }
                 const bool leaf = QN ? walk_box_q(rq, fb, fs, ps.o, inv, w, ptri) : walk_box(rn, ps.o, inv, w, ptri);
                 if (leaf) mode = LANE_TRI;
                 else if (w.pos == w.end) mesh_done();
@@ -333,7 +367,15 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                 if (PROF) { prof[5]++; prof[6] += (unsigned long long)__popcll(pend); }
                 if (mode == LANE_TRI) {
                     if (QN) walk_tri_q(rn, rt, ps.o, ps.d, inv, w, ptri);
-                    else walk_tri(rt, ps.o, ps.d, w, ptri);
+                    else {
+                        if (PT_DUP == 3) {
+                            MeshWalk w2 = w; v3 o2 = ps.o, d2 = ps.d; int t2 = ptri;
+                            opaque(w2); opaque(o2); opaque(d2); opaque(t2);
+                            walk_tri(rt, o2, d2, w2, t2);
+                            opaque(w2);
+                        }
+                        walk_tri(rt, ps.o, ps.d, w, ptri);
+                    }
                     mode = LANE_WALK;
                     if (w.pos == w.end) mesh_done();
                 }
