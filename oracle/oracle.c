@@ -208,6 +208,9 @@ static int mesh_bvh(const or_scene* sc, int m, or_v3 o, or_v3 d, float* ht, floa
         }
     }
     if (hit) { *ht = min_t; *ht1 = min_t1; *ht2 = min_t2; *htri = min_tri; }
+#ifdef OR_STUDY_HOOK
+    OR_STUDY_HOOK(sc, m, o, d, hit, min_t, min_tri);  /* tools/traversal_study.c only */
+#endif
     return hit;
 }
 

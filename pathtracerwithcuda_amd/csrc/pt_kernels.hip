@@ -230,7 +230,7 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
 // PROF: wave-level occupancy counters of the state machine into stats[16..23] (tools/uprof.py):
 // rounds, walk steps, walking lanes summed over steps, shading batches, lanes shaded, triangle
 // batches, lanes in triangle batches, lanes refilled.
-template <int MINW, bool PROF, bool QN>
+template <int MINW, bool PROF, bool QN, int CHAIN>
 __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
                                                                 int walk_steps, int tri_min, int walk_min) {
@@ -356,7 +356,8 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                     bool l2 = walk_box(rn, o2, i2, w2, t2);
                     opaque(w2); opaque(l2); opaque(t2);
                 }
-                const bool leaf = QN ? walk_box_q(rq, fb, fs, ps.o, inv, w, ptri) : walk_box(rn, ps.o, inv, w, ptri);
+                const bool leaf = QN ? walk_box_q(rq, fb, fs, ps.o, inv, w, ptri)
+                                     : (CHAIN > 1 ? walk_box_chain<CHAIN>(rn, ps.o, inv, w, ptri) : walk_box(rn, ps.o, inv, w, ptri));
                 if (leaf) mode = LANE_TRI;
                 else if (w.pos == w.end) mesh_done();
             }
@@ -555,15 +556,15 @@ static PassFn pass_fn(bool leaf1, bool stats, int minw, bool qn) {
     return pass_kernel<false, true, 5, false>;
 }
 
-// PT_MIN_WAVES overrides the occupancy target: 8 waves/SIMD for pass_kernel (64 VGPRs), 5 for
-// pass_kernel_u (96 VGPRs, no spills), the measured optimum of each.
+// PT_MIN_WAVES overrides the occupancy target: 8 waves/SIMD for pass_kernel (64 VGPRs), 6 for
+// pass_kernel_u (80 VGPRs, a few spilled), the measured optimum of each.
 int pass_min_waves(bool unified) {
     static int w = [] {
         const char* e = getenv("PT_MIN_WAVES");
         int v = e ? atoi(e) : 0;
         return (v >= 4 && v <= 8) ? v : 0;
     }();
-    return w ? w : (unified ? 5 : 8);
+    return w ? w : (unified ? 6 : 8);
 }
 
 // PT_UNIFIED=0 selects pass_kernel for the default configuration (leaf size 1, uninstrumented, exact
@@ -575,14 +576,15 @@ bool unified_enabled() {
 
 using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int, int);
 
+// PT_WALK_CHAIN: records per walk step (walk_box_chain); 1 = walk_box.
 static PassFnU pass_fn_u(int minw, bool qn) {
     static const int prof = env_int("PT_UPROF", 0, 0, 1);
-    if (prof) return qn ? pass_kernel_u<5, true, true> : pass_kernel_u<5, true, false>;
-    if (qn) return minw == 6 ? pass_kernel_u<6, false, true> : pass_kernel_u<5, false, true>;
-    if (minw == 6) return pass_kernel_u<6, false, false>;
-    if (minw == 7) return pass_kernel_u<7, false, false>;
-    if (minw == 8) return pass_kernel_u<8, false, false>;
-    return pass_kernel_u<5, false, false>;
+    static const int chain = env_int("PT_WALK_CHAIN", 2, 1, 3);
+    if (prof) return qn ? pass_kernel_u<5, true, true, 1> : pass_kernel_u<5, true, false, 2>;
+    if (qn) return minw == 6 ? pass_kernel_u<6, false, true, 1> : pass_kernel_u<5, false, true, 1>;
+    if (chain == 1) return minw == 6 ? pass_kernel_u<6, false, false, 1> : pass_kernel_u<5, false, false, 1>;
+    if (chain == 3) return minw == 6 ? pass_kernel_u<6, false, false, 3> : pass_kernel_u<5, false, false, 3>;
+    return minw == 6 ? pass_kernel_u<6, false, false, 2> : pass_kernel_u<5, false, false, 2>;
 }
 
 static bool use_unified(bool leaf1, bool stats, bool qn) { (void)qn; return leaf1 && !stats && unified_enabled(); }

@@ -442,6 +442,37 @@ __device__ __forceinline__ bool walk_box(const __amdgpu_buffer_rsrc_t rn, v3 o, 
     return false;
 }
 
+// walk_box over a run of CHAIN consecutive records loaded together (the node and the next CHAIN - 1 in
+// preorder). A passing internal node's successor is pos + 1 (its left child), whose record is then
+// already in registers, so a descent costs no further dependent load. The visited nodes, their
+// order and every test are walk_box's; only more records are fetched per step (the extra ones beyond
+// a failed test are not used).
+template <int CHAIN>
+__device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri) {
+    float4 lo[CHAIN], hi[CHAIN];
+#pragma unroll
+    for (int i = 0; i < CHAIN; i++) {
+        lo[i] = bload(rn, (w.pos + i) * 32);
+        hi[i] = bload(rn, (w.pos + i) * 32 + 16);
+    }
+#pragma unroll
+    for (int i = 0; i < CHAIN; i++) {
+        float entry;
+        if (box_hit(lo[i], hi[i], o, inv, &entry) && entry <= w.t) {
+            const int slot = f2i(hi[i].w);
+            if (slot >= 0) {
+                tri = slot;
+                return true;
+            }
+            w.pos++;
+        } else {
+            w.pos = f2i(lo[i].w);
+            return false;
+        }
+    }
+    return false;
+}
+
 __device__ __forceinline__ void walk_tri(const __amdgpu_buffer_rsrc_t rt, v3 o, v3 d, MeshWalk& w, int tri) {
     float t, t1, t2;
     const float4 a = bload(rt, tri * 48), b = bload(rt, tri * 48 + 16), c = bload(rt, tri * 48 + 32);

@@ -6,7 +6,7 @@ import sys
 
 root = sys.argv[1]
 agg = {}
-for f in glob.glob(os.path.join(root, "*", "run_counter_collection.csv")):
+for f in glob.glob(os.path.join(root, "**", "run_counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0]
         agg.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))

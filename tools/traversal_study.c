@@ -1,0 +1,282 @@
+/*
+ * traversal_study.c — STUDY TOOL (test infrastructure, never linked into the product).
+ *
+ * Builds the oracle with a hook after every mesh walk (oracle.c mesh_bvh, path_tracer_kernel.cu:85-161)
+ * and replays each walked ray through alternative traversals of the SAME BVH, counting the work
+ * they do and every ray whose closest hit differs from the reference's preorder walk:
+ *   oct     — stackless skip-index walk over a per-ray-octant copy of the tree whose children are
+ *             ordered near-first along their split axis; cull `entry <= best`; ties on t broken by
+ *             the reference preorder position of the leaf (the reference keeps the first in preorder).
+ *   octm    — the same with the cull relaxed to entry <= best * (1 + 2^-10) (the detection margin).
+ *   stack   — ordered BVH2 with a stack (test both children, descend the nearer): the ideal order.
+ * An "anomaly" is a candidate triangle (test passes, t > 0) whose computed t lies before its leaf
+ * box's computed entry: the only case in which the accepted hit can depend on visit order.
+ *
+ *   make -C tools study   then   python tools/traversal_study.py
+ */
+#include <stdint.h>
+#include <stdio.h>
+
+struct or_scene_fwd;
+static void study_hook(const void* sc, int m, float ox, float oy, float oz, float dx, float dy, float dz, int hit,
+                       float t, int tri);
+#define OR_STUDY_HOOK(sc, m, o, d, hit, t, tri) study_hook(sc, m, o.x, o.y, o.z, d.x, d.y, d.z, hit, t, tri)
+#include "../oracle/oracle.c"
+
+typedef struct { float lo[3], hi[3]; int skip, tri, orig; } sn;
+typedef struct { int n; int* left; int* right; sn* oct[8]; const pt_bvh_node_device* ref; unsigned long long* visits; } smesh;
+
+#define MAXM 16
+static smesh g_mesh[MAXM];
+static unsigned long long g_stat[16];
+static unsigned long long g_mesh_tris[MAXM], g_mesh_nodes[MAXM], g_mesh_calls[MAXM], g_mesh_oct[MAXM], g_mesh_n[MAXM];
+enum { S_CALLS, S_REF_NODES, S_OCT_NODES, S_OCTM_NODES, S_STACK_BOX, S_STACK_POPS, S_OCT_MISMATCH, S_OCTM_MISMATCH,
+       S_ANOM, S_TIE, S_STACK_MISMATCH, S_REF_HITS, S_NSTAT };
+
+static void cen(const pt_bounding_box* b, float c[3]) {
+    c[0] = 0.5f * (b->left_bottom.x + b->right_top.x);
+    c[1] = 0.5f * (b->left_bottom.y + b->right_top.y);
+    c[2] = 0.5f * (b->left_bottom.z + b->right_top.z);
+}
+
+static int emit(smesh* s, int k, int pos, int out, sn* arr) {
+    const pt_bvh_node_device* nd = &s->ref[pos];
+    sn* e = &arr[out];
+    e->lo[0] = nd->box.left_bottom.x; e->lo[1] = nd->box.left_bottom.y; e->lo[2] = nd->box.left_bottom.z;
+    e->hi[0] = nd->box.right_top.x; e->hi[1] = nd->box.right_top.y; e->hi[2] = nd->box.right_top.z;
+    e->orig = pos;
+    if (nd->is_leaf) {
+        e->tri = nd->triangle_indices[0];
+        e->skip = out + 1;
+        return out + 1;
+    }
+    e->tri = -1;
+    int l = s->left[pos], r = s->right[pos];
+    float cl[3], cr[3];
+    cen(&s->ref[l].box, cl);
+    cen(&s->ref[r].box, cr);
+    int ax = 0;
+    float best = -1.0f;
+    for (int a = 0; a < 3; a++) {
+        float dd = fabsf(cl[a] - cr[a]);
+        if (dd > best) { best = dd; ax = a; }
+    }
+    int neg = (k >> ax) & 1;  /* ray direction negative on the axis: visit the higher child first */
+    int first = l, second = r;
+    if ((cl[ax] > cr[ax]) != neg) { first = r; second = l; }
+    int nx = emit(s, k, first, out + 1, arr);
+    nx = emit(s, k, second, nx, arr);
+    e->skip = nx;
+    return nx;
+}
+
+static void prepare(const or_scene* sc, int m) {
+    smesh* s = &g_mesh[m];
+    if (s->n) return;
+    const pt_bvh_node_device* nodes = sc->bvh[m];
+    int n = nodes[0].next_node_index;
+    s->ref = nodes;
+    s->left = malloc(sizeof(int) * n);
+    s->right = malloc(sizeof(int) * n);
+    s->visits = calloc(n, sizeof(unsigned long long));
+    for (int p = 0; p < n; p++) {
+        if (nodes[p].is_leaf) { s->left[p] = s->right[p] = -1; continue; }
+        s->left[p] = p + 1;
+        s->right[p] = nodes[p + 1].next_node_index;
+    }
+    for (int k = 0; k < 8; k++) {
+        s->oct[k] = malloc(sizeof(sn) * n);
+        int e = emit(s, k, 0, 0, s->oct[k]);
+        if (e != n) { fprintf(stderr, "emit %d != %d\n", e, n); abort(); }
+    }
+    __atomic_store_n(&s->n, n, __ATOMIC_RELEASE);
+}
+
+static int sbox(const float lo[3], const float hi[3], or_v3 o, or_v3 inv, float* entry) {
+    float tx1 = (lo[0] - o.x) * inv.x, tx2 = (hi[0] - o.x) * inv.x;
+    float ty1 = (lo[1] - o.y) * inv.y, ty2 = (hi[1] - o.y) * inv.y;
+    float tz1 = (lo[2] - o.z) * inv.z, tz2 = (hi[2] - o.z) * inv.z;
+    float t_max = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    float t_min = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    *entry = t_max;
+    return t_max <= t_min && t_min > 0.0f;
+}
+
+typedef struct { float t; int tri, orig; } best_t;
+
+static void candidate(const or_scene* sc, int tri, int orig, float entry, or_v3 o, or_v3 d, best_t* b,
+                      unsigned long long* anom, unsigned long long* tie) {
+    float t, t1, t2;
+    if (!triangle_intersect(&sc->tris[tri], o, d, &t, &t1, &t2) || !(t > 0.0f)) return;
+    if (entry > t) (*anom)++;
+    if (t < b->t || (t == b->t && orig < b->orig)) {
+        if (t == b->t) (*tie)++;
+        b->t = t; b->tri = tri; b->orig = orig;
+    }
+}
+
+static void walk_oct(const or_scene* sc, const smesh* s, int k, or_v3 o, or_v3 d, or_v3 inv, float margin, best_t* b,
+                     unsigned long long* nodes, unsigned long long* anom, unsigned long long* tie) {
+    const sn* a = s->oct[k];
+    int pos = 0;
+    b->t = INFINITY; b->tri = -1; b->orig = 0x7fffffff;
+    while (pos != s->n) {
+        const sn* e = &a[pos];
+        float entry;
+        (*nodes)++;
+        if (sbox(e->lo, e->hi, o, inv, &entry) && entry <= b->t * margin) {
+            if (e->tri >= 0) candidate(sc, e->tri, e->orig, entry, o, d, b, anom, tie);
+            pos++;
+        } else {
+            pos = e->skip;
+        }
+    }
+}
+
+static void walk_stack(const or_scene* sc, const smesh* s, or_v3 o, or_v3 d, or_v3 inv, best_t* b,
+                       unsigned long long* boxes, unsigned long long* pops) {
+    int stk[256];
+    float ent[256];
+    int sp = 0;
+    unsigned long long an = 0, ti = 0;
+    b->t = INFINITY; b->tri = -1; b->orig = 0x7fffffff;
+    const pt_bvh_node_device* nd = s->ref;
+    float e0;
+    (*boxes)++;
+    float lo[3] = {nd[0].box.left_bottom.x, nd[0].box.left_bottom.y, nd[0].box.left_bottom.z};
+    float hi[3] = {nd[0].box.right_top.x, nd[0].box.right_top.y, nd[0].box.right_top.z};
+    if (!sbox(lo, hi, o, inv, &e0)) return;
+    stk[sp] = 0; ent[sp] = e0; sp++;
+    while (sp) {
+        sp--;
+        int p = stk[sp];
+        if (ent[sp] > b->t) continue;
+        (*pops)++;
+        if (nd[p].is_leaf) {
+            candidate(sc, nd[p].triangle_indices[0], p, ent[sp], o, d, b, &an, &ti);
+            continue;
+        }
+        int c[2] = {s->left[p], s->right[p]};
+        float ce[2];
+        int h[2];
+        for (int i = 0; i < 2; i++) {
+            const pt_bounding_box* bb = &nd[c[i]].box;
+            float l3[3] = {bb->left_bottom.x, bb->left_bottom.y, bb->left_bottom.z};
+            float h3[3] = {bb->right_top.x, bb->right_top.y, bb->right_top.z};
+            (*boxes)++;
+            h[i] = sbox(l3, h3, o, inv, &ce[i]) && ce[i] <= b->t;
+        }
+        int nearf = (h[0] && h[1]) ? (ce[1] < ce[0]) : (h[1] ? 1 : 0);
+        int farf = 1 - nearf;
+        if (h[farf]) { stk[sp] = c[farf]; ent[sp] = ce[farf]; sp++; }
+        if (h[nearf]) { stk[sp] = c[nearf]; ent[sp] = ce[nearf]; sp++; }
+        if (sp > 250) abort();
+    }
+}
+
+static void study_hook(const void* scv, int m, float ox, float oy, float oz, float dx, float dy, float dz, int hit,
+                       float t, int tri) {
+    const or_scene* sc = (const or_scene*)scv;
+    if (m >= MAXM) return;
+    smesh* s = &g_mesh[m];
+    if (!__atomic_load_n(&s->n, __ATOMIC_ACQUIRE)) {
+#pragma omp critical(study_prep)
+        prepare(sc, m);
+    }
+    or_v3 o = v3(ox, oy, oz), d = v3(dx, dy, dz);
+    or_v3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    int k = (d.x < 0.0f) | ((d.y < 0.0f) << 1) | ((d.z < 0.0f) << 2);
+    unsigned long long loc[S_NSTAT] = {0};
+    loc[S_CALLS] = 1;
+    loc[S_REF_HITS] = hit ? 1 : 0;
+    /* reference node count: the preorder walk again (cheap to recount here) */
+    {
+        best_t b;
+        unsigned long long an = 0, ti = 0;
+        const pt_bvh_node_device* nd = s->ref;
+        int pos = 0;
+        b.t = INFINITY; b.tri = -1; b.orig = 0x7fffffff;
+        while (pos != s->n) {
+            float lo[3] = {nd[pos].box.left_bottom.x, nd[pos].box.left_bottom.y, nd[pos].box.left_bottom.z};
+            float hi[3] = {nd[pos].box.right_top.x, nd[pos].box.right_top.y, nd[pos].box.right_top.z};
+            float e;
+            loc[S_REF_NODES]++;
+            __atomic_fetch_add(&s->visits[pos], 1, __ATOMIC_RELAXED);
+            if (sbox(lo, hi, o, inv, &e) && e <= b.t) {
+                if (nd[pos].is_leaf) {
+                    float tt, t1, t2;
+                    __atomic_fetch_add(&g_mesh_tris[m], 1, __ATOMIC_RELAXED);
+                    int ti2 = nd[pos].triangle_indices[0];
+                    if (triangle_intersect(&sc->tris[ti2], o, d, &tt, &t1, &t2) && tt > 0.0f && tt < b.t) {
+                        b.t = tt; b.tri = ti2;
+                    }
+                }
+                pos++;
+            } else pos = nd[pos].next_node_index;
+        }
+        (void)an; (void)ti;
+    }
+    best_t b;
+    walk_oct(sc, s, k, o, d, inv, 1.0f, &b, &loc[S_OCT_NODES], &loc[S_ANOM], &loc[S_TIE]);
+    int same = hit ? (b.tri == tri && b.t == t) : (b.tri < 0);
+    if (!same) loc[S_OCT_MISMATCH]++;
+    unsigned long long dummy = 0;
+    walk_oct(sc, s, k, o, d, inv, 1.0f + 1.0f / 1024.0f, &b, &loc[S_OCTM_NODES], &dummy, &dummy);
+    same = hit ? (b.tri == tri && b.t == t) : (b.tri < 0);
+    if (!same) loc[S_OCTM_MISMATCH]++;
+    walk_stack(sc, s, o, d, inv, &b, &loc[S_STACK_BOX], &loc[S_STACK_POPS]);
+    same = hit ? (b.tri == tri && b.t == t) : (b.tri < 0);
+    if (!same) loc[S_STACK_MISMATCH]++;
+    for (int i = 0; i < S_NSTAT; i++) __atomic_fetch_add(&g_stat[i], loc[i], __ATOMIC_RELAXED);
+    __atomic_fetch_add(&g_mesh_nodes[m], loc[S_REF_NODES], __ATOMIC_RELAXED);
+    __atomic_fetch_add(&g_mesh_oct[m], loc[S_OCT_NODES], __ATOMIC_RELAXED);
+    __atomic_fetch_add(&g_mesh_calls[m], 1, __ATOMIC_RELAXED);
+    g_mesh_n[m] = s->n;
+}
+
+
+static double sa(const pt_bounding_box* b) {
+    double x = b->right_top.x - b->left_bottom.x, y = b->right_top.y - b->left_bottom.y, z = b->right_top.z - b->left_bottom.z;
+    return x * y + y * z + z * x;
+}
+/* share of visits landing on a top tree of `budget` nodes: BFS levels, or greedy by surface area */
+static void coverage(smesh* s, int budget) {
+    int n = s->n;
+    unsigned long long tot = 0;
+    for (int p = 0; p < n; p++) tot += s->visits[p];
+    char* in = calloc(n, 1);
+    int cnt = 1;
+    in[0] = 1;
+    /* greedy: repeatedly expand the top-leaf internal node of largest surface area */
+    while (cnt + 2 <= budget) {
+        int bestp = -1; double bs = -1;
+        for (int p = 0; p < n; p++)
+            if (in[p] && s->left[p] >= 0 && !in[s->left[p]]) { double a = sa(&s->ref[p].box); if (a > bs) { bs = a; bestp = p; } }
+        if (bestp < 0) break;
+        in[s->left[bestp]] = in[s->right[bestp]] = 1; cnt += 2;
+    }
+    unsigned long long cov = 0;
+    for (int p = 0; p < n; p++) if (in[p]) cov += s->visits[p];
+    /* BFS */
+    char* in2 = calloc(n, 1);
+    int* q = malloc(sizeof(int) * n); int qh = 0, qt = 0, c2 = 1; q[qt++] = 0; in2[0] = 1;
+    while (qh < qt) { int p = q[qh++]; if (s->left[p] < 0) continue; if (c2 + 2 > budget) break;
+        in2[s->left[p]] = in2[s->right[p]] = 1; c2 += 2; q[qt++] = s->left[p]; q[qt++] = s->right[p]; }
+    unsigned long long cov2 = 0;
+    for (int p = 0; p < n; p++) if (in2[p]) cov2 += s->visits[p];
+    printf("    budget %5d: SA-greedy %d nodes cover %.3f of visits; BFS %d nodes cover %.3f\n", budget, cnt,
+           (double)cov / tot, c2, (double)cov2 / tot);
+    free(in); free(in2); free(q);
+}
+
+void study_stats(unsigned long long* out) {
+    for (int m = 0; m < MAXM; m++)
+        if (g_mesh[m].n > 1000) { int b[] = {64, 128, 256, 512, 1024, 2048, 4096}; for (int i = 0; i < 7; i++) coverage(&g_mesh[m], b[i]); }
+    for (int i = 0; i < S_NSTAT; i++) out[i] = g_stat[i];
+    for (int m = 0; m < MAXM; m++)
+        if (g_mesh_calls[m])
+            printf("  mesh %d: %llu nodes, %llu walks, ref nodes/walk %.2f, tris/walk %.2f, oct nodes/walk %.2f\n", m,
+                   g_mesh_n[m], g_mesh_calls[m], (double)g_mesh_nodes[m] / g_mesh_calls[m],
+                   (double)g_mesh_tris[m] / g_mesh_calls[m], (double)g_mesh_oct[m] / g_mesh_calls[m]);
+    fflush(stdout);
+}

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""STUDY TOOL: alternative BVH traversal orders replayed on the rays of the bench frame
+(tools/traversal_study.c). Prints work counts and closest-hit mismatches against the reference's
+preorder walk. CPU only; test infrastructure (uses the oracle)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import bench  # noqa: E402  (scene constants)
+import oracle  # noqa: E402
+import pathtracerwithcuda_amd as pt  # noqa: E402
+
+NAMES = ["calls", "ref_nodes", "oct_nodes", "octm_nodes", "stack_boxes", "stack_pops", "oct_mismatch",
+         "octm_mismatch", "anomalies", "ties", "stack_mismatch", "ref_hits"]
+
+
+def main():
+    sample = int(sys.argv[1]) if len(sys.argv) > 1 else 100000
+    passes = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    so = "/tmp/libstudy.so"
+    subprocess.run(["gcc", "-O2", "-std=gnu11", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fopenmp",
+                    "-shared", os.path.join(ROOT, "tools", "traversal_study.c"), "-o", so, "-lm"], check=True)
+    oracle.build()
+    oracle.LIB = so
+    L = oracle.lib()
+    L.study_stats.argtypes = [C.c_void_p]
+    scene = pt.cornell_scene(pt.torus_knot(*bench.KNOT))
+    cfg = pt.configuration(max_tracer_depth=bench.DEPTH)
+    cam = pt.camera(bench.WIDTH, bench.HEIGHT, **bench.CAMERA)
+    rng = np.random.default_rng(1)
+    pix = np.sort(rng.choice(bench.WIDTH * bench.HEIGHT, size=sample, replace=False)).astype(np.int32)
+    t0 = time.time()
+    oracle.render(scene.view, cam, cfg, 1, passes, pixels=pix, with_u8=False)
+    st = (C.c_ulonglong * 16)()
+    L.study_stats(st)
+    d = dict(zip(NAMES, list(st)[:len(NAMES)]))
+    c = max(d["calls"], 1)
+    print(f"{sample} px x {passes} passes, {time.time() - t0:.1f} s")
+    for k, v in d.items():
+        print(f"  {k:15s} {v:14d}  per walk {v / c:8.3f}")
+    print(f"  oct/ref nodes {d['oct_nodes'] / d['ref_nodes']:.3f}  octm/ref {d['octm_nodes'] / d['ref_nodes']:.3f}"
+          f"  stack pops/ref {d['stack_pops'] / d['ref_nodes']:.3f}  stack boxes/ref {d['stack_boxes'] / d['ref_nodes']:.3f}")
+
+
+if __name__ == "__main__":
+    main()
