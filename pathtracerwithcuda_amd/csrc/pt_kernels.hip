@@ -230,7 +230,7 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
 // PROF: wave-level occupancy counters of the state machine into stats[16..23] (tools/uprof.py):
 // rounds, walk steps, walking lanes summed over steps, shading batches, lanes shaded, triangle
 // batches, lanes in triangle batches, lanes refilled.
-template <int MINW, bool PROF, bool QN, int CHAIN>
+template <int MINW, bool PROF, bool QN, int CHAIN, bool PF>
 __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
                                                                 int walk_steps, int tri_min, int walk_min) {
@@ -346,6 +346,9 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
             mesh++;
             mode = start_mesh(sc, mesh, w) ? LANE_WALK : LANE_READY;
         };
+        // PF: the parked triangle's geometry, loaded at the park; scoped to the walk loop, which no lane
+        // leaves parked (the last step flushes the batch), so it is not live across shading
+        float4 pta = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ptb = pta, ptc = pta;
         for (int k = 0; k < walk_steps; k++) {
             if (k > 0 && !__any(mode == LANE_WALK || mode == LANE_TRI)) break;
             if (PROF) { prof[1]++; prof[2] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK)); }
@@ -358,13 +361,21 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                 }
                 const bool leaf = QN ? walk_box_q(rq, fb, fs, ps.o, inv, w, ptri)
                                      : (CHAIN > 1 ? walk_box_chain<CHAIN>(rn, ps.o, inv, w, ptri) : walk_box(rn, ps.o, inv, w, ptri));
-                if (leaf) mode = LANE_TRI;
-                else if (w.pos == w.end) mesh_done();
+                if (leaf) {
+                    mode = LANE_TRI;
+                    if (PF && !QN) {  // the triangle's loads are in flight while the batch fills
+                        pta = bload(rt, ptri * 48); ptb = bload(rt, ptri * 48 + 16); ptc = bload(rt, ptri * 48 + 32);
+                    }
+                } else if (w.pos == w.end) {
+                    mesh_done();
+                }
             }
             // leaf triangles are tested in batches of at least tri_min lanes (or when no lane can
             // walk on): the triangle test then runs with many lanes active instead of one or two
             const unsigned long long pend = __ballot(mode == LANE_TRI);
-            if (pend && (__popcll(pend) >= (unsigned int)tri_min || !__any(mode == LANE_WALK))) {
+            // PF: no lane leaves the walk loop parked, so the prefetched geometry never lives across shading
+            if (pend && (__popcll(pend) >= (unsigned int)tri_min || !__any(mode == LANE_WALK) ||
+                         (PF && k == walk_steps - 1))) {
                 if (PROF) { prof[5]++; prof[6] += (unsigned long long)__popcll(pend); }
                 if (mode == LANE_TRI) {
                     if (QN) walk_tri_q(rn, rt, ps.o, ps.d, inv, w, ptri);
@@ -375,7 +386,8 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                             walk_tri(rt, o2, d2, w2, t2);
                             opaque(w2);
                         }
-                        walk_tri(rt, ps.o, ps.d, w, ptri);
+                        if (PF) walk_tri_geom(pta, ptb, ptc, ps.o, ps.d, w, ptri);
+                        else walk_tri(rt, ps.o, ps.d, w, ptri);
                     }
                     mode = LANE_WALK;
                     if (w.pos == w.end) mesh_done();
@@ -580,11 +592,13 @@ using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int,
 static PassFnU pass_fn_u(int minw, bool qn) {
     static const int prof = env_int("PT_UPROF", 0, 0, 1);
     static const int chain = env_int("PT_WALK_CHAIN", 2, 1, 3);
-    if (prof) return qn ? pass_kernel_u<5, true, true, 1> : pass_kernel_u<5, true, false, 2>;
-    if (qn) return minw == 6 ? pass_kernel_u<6, false, true, 1> : pass_kernel_u<5, false, true, 1>;
-    if (chain == 1) return minw == 6 ? pass_kernel_u<6, false, false, 1> : pass_kernel_u<5, false, false, 1>;
-    if (chain == 3) return minw == 6 ? pass_kernel_u<6, false, false, 3> : pass_kernel_u<5, false, false, 3>;
-    return minw == 6 ? pass_kernel_u<6, false, false, 2> : pass_kernel_u<5, false, false, 2>;
+    static const int pf = env_int("PT_TRI_PREFETCH", 1, 0, 1);
+    if (prof) return qn ? pass_kernel_u<6, true, true, 1, false> : pass_kernel_u<6, true, false, 2, true>;
+    if (qn) return minw == 6 ? pass_kernel_u<6, false, true, 1, false> : pass_kernel_u<5, false, true, 1, false>;
+    if (chain == 1) return minw == 6 ? pass_kernel_u<6, false, false, 1, false> : pass_kernel_u<5, false, false, 1, false>;
+    if (chain == 3) return minw == 6 ? pass_kernel_u<6, false, false, 3, false> : pass_kernel_u<5, false, false, 3, false>;
+    if (pf) return minw == 6 ? pass_kernel_u<6, false, false, 2, true> : pass_kernel_u<5, false, false, 2, true>;
+    return minw == 6 ? pass_kernel_u<6, false, false, 2, false> : pass_kernel_u<5, false, false, 2, false>;
 }
 
 static bool use_unified(bool leaf1, bool stats, bool qn) { (void)qn; return leaf1 && !stats && unified_enabled(); }

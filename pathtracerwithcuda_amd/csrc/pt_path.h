@@ -473,6 +473,15 @@ __device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, 
     return false;
 }
 
+// walk_tri with the triangle's records already loaded.
+__device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri) {
+    float t, t1, t2;
+    if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t) {
+        w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
+    }
+    w.pos++;
+}
+
 __device__ __forceinline__ void walk_tri(const __amdgpu_buffer_rsrc_t rt, v3 o, v3 d, MeshWalk& w, int tri) {
     float t, t1, t2;
     const float4 a = bload(rt, tri * 48), b = bload(rt, tri * 48 + 16), c = bload(rt, tri * 48 + 32);
