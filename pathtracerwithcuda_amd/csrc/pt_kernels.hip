@@ -176,11 +176,21 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
 // same tests, same draws keyed by (pass, pixel, depth)); only the interleaving between lanes changes.
 enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3, LANE_TRI = 4 };
 
-// Starts the walk of the first mesh at or after `mesh` with a non-empty node range.
-__device__ __forceinline__ bool start_mesh(const DevScene& sc, int& mesh, MeshWalk& w) {
-    const int2* mr = uniform_ptr(sc.mesh_range);
+// Starts the walk of the first mesh at or after `mesh` with a non-empty node range. The ranges of the
+// first PT_LDS_MESHES meshes come from the workgroup's LDS copy (lds_mesh, filled at kernel start), the
+// rest from global memory.
+#define PT_LDS_MESHES 64
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bool start_mesh(const DevScene& sc, const int2* lds_mesh, int& mesh, MeshWalk& w) {
     while (mesh < sc.mesh_num) {
-        const int2 r = mr[mesh];
+        int2 r;
+        if (mesh < PT_LDS_MESHES) {
+            r = lds_mesh[mesh];
+        } else {  // a buffer load (not a pointer select that would turn both into flat loads)
+            const i32x2 v = __builtin_bit_cast(i32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                make_rsrc(sc.mesh_range, sc.mesh_num * 8), mesh * 8, 0, 0));
+            r.x = v.x; r.y = v.y;
+        }
         if (r.x != r.y) {
             w.pos = r.x; w.end = r.y;
             w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
@@ -193,8 +203,8 @@ __device__ __forceinline__ bool start_mesh(const DevScene& sc, int& mesh, MeshWa
 
 // Start of one trace_ray_kernel invocation (path_tracer_kernel.cu:418-454): brute-force spheres into
 // the closest hit, then the walk of mesh 0.
-__device__ __forceinline__ int begin_segment(const DevScene& sc, const PathState& ps, v3& inv, Hit& h, MeshWalk& w,
-                                             int& mesh) {
+__device__ __forceinline__ int begin_segment(const DevScene& sc, const int2* lds_mesh, const PathState& ps, v3& inv,
+                                             Hit& h, MeshWalk& w, int& mesh) {
     h.t = __builtin_inff(); h.t1 = __builtin_inff(); h.t2 = __builtin_inff();
     h.type = 0; h.prim = -1;
     for (int i = 0; i < sc.sphere_num; i++) {
@@ -205,7 +215,7 @@ __device__ __forceinline__ int begin_segment(const DevScene& sc, const PathState
     }
     mesh = 0;
     if (sc.mesh_num > 0) inv = 1.0f / ps.d;
-    return start_mesh(sc, mesh, w) ? LANE_WALK : LANE_READY;
+    return start_mesh(sc, lds_mesh, mesh, w) ? LANE_WALK : LANE_READY;
 }
 
 // pixel_256_transform_gamma_corrected_kernel (:644-680) for one finished (pixel, pass) unit
@@ -238,6 +248,13 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
     const LaunchParams* P0 = params;
     const float clamp_hi = (float)P0->cfg.max_depth * 2.0f;
     const unsigned long long lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    __shared__ int2 lds_mesh[PT_LDS_MESHES];
+    {
+        const int2* mr = uniform_ptr(P0->sc.mesh_range);
+        const int n = min(uniform_int(P0->sc.mesh_num), PT_LDS_MESHES);
+        for (int i = threadIdx.x; i < n; i += PT_BLOCK) lds_mesh[i] = mr[i];
+        __syncthreads();
+    }
 
     PathState ps;
     v3 inv = mk3(0.0f, 0.0f, 0.0f);
@@ -291,7 +308,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                     pseed = path_seed(hseed, pixel);
                     depth = 0;
                     if (cfg.max_depth > 0) {
-                        mode = begin_segment(sc, ps, inv, h, w, mesh);
+                        mode = begin_segment(sc, lds_mesh, ps, inv, h, w, mesh);
                     } else {
                         finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
                     }
@@ -322,7 +339,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                     finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
                     mode = LANE_WANT;
                 } else {
-                    mode = begin_segment(sc, ps, inv, h, w, mesh);
+                    mode = begin_segment(sc, lds_mesh, ps, inv, h, w, mesh);
                 }
             }
             if (PROF) prof[9] += __builtin_readcyclecounter() - tc;
@@ -344,7 +361,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                 h.t = w.t; h.t1 = w.t1; h.t2 = w.t2; h.prim = w.tri; h.type = 2;
             }
             mesh++;
-            mode = start_mesh(sc, mesh, w) ? LANE_WALK : LANE_READY;
+            mode = start_mesh(sc, lds_mesh, mesh, w) ? LANE_WALK : LANE_READY;
         };
         // PF: the parked triangle's geometry, loaded at the park; scoped to the walk loop, which no lane
         // leaves parked (the last step flushes the batch), so it is not live across shading
