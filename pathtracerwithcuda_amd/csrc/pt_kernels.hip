@@ -248,11 +248,18 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
     const LaunchParams* P0 = params;
     const float clamp_hi = (float)P0->cfg.max_depth * 2.0f;
     const unsigned long long lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    // workgroup copies in LDS: the first mesh ranges and every material (the launch reserves
+    // material_num * sizeof(DevMaterial) bytes of dynamic LDS; pass_kernel_u runs only when that fits)
     __shared__ int2 lds_mesh[PT_LDS_MESHES];
+    extern __shared__ float4 lds_dyn[];
+    DevMaterial* lds_mats = reinterpret_cast<DevMaterial*>(lds_dyn);
     {
         const int2* mr = uniform_ptr(P0->sc.mesh_range);
         const int n = min(uniform_int(P0->sc.mesh_num), PT_LDS_MESHES);
         for (int i = threadIdx.x; i < n; i += PT_BLOCK) lds_mesh[i] = mr[i];
+        const float4* ms = reinterpret_cast<const float4*>(uniform_ptr(P0->sc.materials));
+        const int nm = uniform_int(P0->sc.material_num) * (int)(sizeof(DevMaterial) / 16);
+        for (int i = threadIdx.x; i < nm; i += PT_BLOCK) lds_dyn[i] = ms[i];
         __syncthreads();
     }
 
@@ -279,7 +286,8 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
         const LaunchParams* P = params;
         asm volatile("" : "+s"(P));
         P = uniform_ptr(P);
-        const DevScene sc = load_const(&P->sc);
+        DevScene sc = load_const(&P->sc);
+        sc.materials = lds_mats;
         const DevConfig cfg = load_const(&P->cfg);
         const DevTiling til = load_const(&P->til);
         const DevOutput out = load_const(&P->out);
@@ -618,11 +626,16 @@ static PassFnU pass_fn_u(int minw, bool qn) {
     return minw == 6 ? pass_kernel_u<6, false, false, 2, false> : pass_kernel_u<5, false, false, 2, false>;
 }
 
-static bool use_unified(bool leaf1, bool stats, bool qn) { (void)qn; return leaf1 && !stats && unified_enabled(); }
+// pass_kernel_u keeps every material in LDS: scenes with more than PT_LDS_MATERIALS run pass_kernel.
+#define PT_LDS_MATERIALS 256
+static bool use_unified(bool leaf1, bool stats, bool qn, int material_num) {
+    (void)qn;
+    return leaf1 && !stats && unified_enabled() && material_num <= PT_LDS_MATERIALS;
+}
 
 hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int first_pass, int batch_log2,
-                       int write_u8, int grid, bool stats, hipStream_t stream) {
-    if (use_unified(leaf1, stats, qn)) {
+                       int write_u8, int grid, bool stats, int material_num, hipStream_t stream) {
+    if (use_unified(leaf1, stats, qn, material_num)) {
         static const int chunk = env_int("PT_CHUNK_MEGA", 0, 0, 4096);
         static const int shade_min = env_int("PT_SHADE_MIN", 40, 1, 64);
         static const int walk_steps = env_int("PT_WALK_STEPS", 12, 1, 64);
@@ -632,8 +645,8 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int 
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
             a8 = walk_min;
         void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8};
-        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn), dim3(grid), dim3(PT_BLOCK), args, 0,
-                                       stream);
+        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn), dim3(grid), dim3(PT_BLOCK), args,
+                                       (size_t)material_num * sizeof(DevMaterial), stream);
         if (e != hipSuccess) return e;
         return hipGetLastError();
     }
@@ -663,13 +676,15 @@ hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256
     return hipGetLastError();
 }
 
-int pass_grid_size(bool leaf1, bool stats, bool qn) {
+int pass_grid_size(bool leaf1, bool stats, bool qn, int material_num) {
     int dev = 0, cus = 0, blocks = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* fn = use_unified(leaf1, stats, qn) ? (const void*)pass_fn_u(pass_min_waves(true), qn)
-                                                   : (const void*)pass_fn(leaf1, stats, pass_min_waves(false), qn);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, PT_BLOCK, 0) != hipSuccess || blocks <= 0) blocks = 4;
+    const bool u = use_unified(leaf1, stats, qn, material_num);
+    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true), qn)
+                       : (const void*)pass_fn(leaf1, stats, pass_min_waves(false), qn);
+    const size_t lds = u ? (size_t)material_num * sizeof(DevMaterial) : 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, PT_BLOCK, lds) != hipSuccess || blocks <= 0) blocks = 4;
     if (cus <= 0) cus = 256;
     return cus * blocks;
 }

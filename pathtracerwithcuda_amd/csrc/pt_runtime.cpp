@@ -414,11 +414,13 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     s.cube_len = st.cube_len;
     s.node_count = (int)(st.nodes.size() / 2);
     s.tri_count = (int)(st.tri_geom.size() / 3);
+    s.material_num = (int)st.mats.size();
     ctx->node_num = (int)(st.nodes.size() / 2);
     ctx->tri_num = (int)(st.tri_geom.size() / 3);
     ctx->material_num = (int)st.mats.size();
     ctx->mat_air_n_valid = false;
     ctx->has_scene = true;
+    std::memset(ctx->grid, 0, sizeof(ctx->grid));  // occupancy depends on the LDS material table
     return PT_OK;
 }
 
@@ -478,7 +480,7 @@ bool use_qnodes(const pt_context* ctx) {
 int pass_grid(pt_context* ctx) {
     const bool leaf1 = ctx->scene.leaf_size == 1, qn = use_qnodes(ctx);
     int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0][qn ? 1 : 0];
-    if (g == 0) g = pass_grid_size(leaf1, ctx->instrumented, qn);
+    if (g == 0) g = pass_grid_size(leaf1, ctx->instrumented, qn, ctx->material_num);
     return g;
 }
 
@@ -645,7 +647,7 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         int rc = ev_begin(ctx, 0);
         if (rc != PT_OK) return rc;
         PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, use_qnodes(ctx), first, lg, w8, grid,
-                           ctx->instrumented, ctx->stream));
+                           ctx->instrumented, ctx->material_num, ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         if (lg > 0) {
             if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;

@@ -75,6 +75,7 @@ struct DevScene {
     int cube_len;
     int node_count;  // records in `nodes` (2 float4 each); bounds of the node buffer descriptor
     int tri_count;   // records in `tri_geom` (3 float4 each)
+    int material_num;  // records in `materials`
 };
 
 // The subset of Core/configuration.h:9-34 that the kernel reads.
