@@ -17,6 +17,7 @@ P="python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$TAG/trace -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/$TAG/trace.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/$TAG/pmc_fetch -o run -- $P > gpurun_out/$TAG/pmc_fetch.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/$TAG/pmc_write -o run -- $P > gpurun_out/$TAG/pmc_write.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/$TAG/pmc_sq -o run -- $P > gpurun_out/$TAG/pmc_sq.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$TAG/wave/trace -o run -- $P --schedule wavefront > gpurun_out/$TAG/wave/trace.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/$TAG/wave/pmc_fetch -o run -- $P --schedule wavefront > gpurun_out/$TAG/wave/pmc_fetch.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/$TAG/wave/pmc_write -o run -- $P --schedule wavefront > gpurun_out/$TAG/wave/pmc_write.log 2>&1 || exit $?

@@ -17,7 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("src")
 ap.add_argument("out")
 ap.add_argument("--workload", default=None)
-ap.add_argument("--kernel", default="pass_kernel_u<5, false, false>")
+ap.add_argument("--kernel", default="pass_kernel_u<6, false, false, 2, true>")
 ap.add_argument("--round", default=None)
 args = ap.parse_args()
 
