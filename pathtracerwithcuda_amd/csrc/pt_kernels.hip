@@ -636,7 +636,7 @@ static bool use_unified(bool leaf1, bool stats, bool qn, int material_num) {
 hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int first_pass, int batch_log2,
                        int write_u8, int grid, bool stats, int material_num, hipStream_t stream) {
     if (use_unified(leaf1, stats, qn, material_num)) {
-        static const int chunk = env_int("PT_CHUNK_MEGA", 0, 0, 4096);
+        static const int chunk = env_int("PT_CHUNK_MEGA", 32, 0, 4096);
         static const int shade_min = env_int("PT_SHADE_MIN", 40, 1, 64);
         static const int walk_steps = env_int("PT_WALK_STEPS", 10, 1, 64);
         const LaunchParams* a0 = params_dev;
@@ -652,7 +652,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int 
     }
     PassFn fn = pass_fn(leaf1, stats, pass_min_waves(false), qn);
     const LaunchParams* a0 = params_dev;
-    static const int chunk = env_int("PT_CHUNK_MEGA", 0, 0, 4096);
+    static const int chunk = env_int("PT_CHUNK_MEGA", 32, 0, 4096);
     int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2;
     void* args[] = {&a0, &a1, &a2, &a3, &a4};
     hipError_t e = hipLaunchKernel((const void*)fn, dim3(grid), dim3(PT_BLOCK), args, 0, stream);
