@@ -637,7 +637,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int 
                        int write_u8, int grid, bool stats, int material_num, hipStream_t stream) {
     if (use_unified(leaf1, stats, qn, material_num)) {
         static const int chunk = env_int("PT_CHUNK_MEGA", 32, 0, 4096);
-        static const int shade_min = env_int("PT_SHADE_MIN", 40, 1, 64);
+        static const int shade_min = env_int("PT_SHADE_MIN", 32, 1, 64);
         static const int walk_steps = env_int("PT_WALK_STEPS", 10, 1, 64);
         const LaunchParams* a0 = params_dev;
         static const int tri_min = env_int("PT_TRI_MIN", 4, 1, 64);
