@@ -448,29 +448,41 @@ __device__ __forceinline__ bool walk_box(const __amdgpu_buffer_rsrc_t rn, v3 o, 
 // order and every test are walk_box's; only more records are fetched per step (the extra ones beyond
 // a failed test are not used).
 template <int CHAIN>
-__device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri) {
+struct ChainRecs {
     float4 lo[CHAIN], hi[CHAIN];
+};
+template <int CHAIN>
+__device__ __forceinline__ void chain_load(const __amdgpu_buffer_rsrc_t rn, int pos, ChainRecs<CHAIN>& r) {
 #pragma unroll
     for (int i = 0; i < CHAIN; i++) {
-        lo[i] = bload(rn, (w.pos + i) * 32);
-        hi[i] = bload(rn, (w.pos + i) * 32 + 16);
+        r.lo[i] = bload(rn, (pos + i) * 32);
+        r.hi[i] = bload(rn, (pos + i) * 32 + 16);
     }
+}
+template <int CHAIN>
+__device__ __forceinline__ bool chain_test(const ChainRecs<CHAIN>& r, v3 o, v3 inv, MeshWalk& w, int& tri) {
 #pragma unroll
     for (int i = 0; i < CHAIN; i++) {
         float entry;
-        if (box_hit(lo[i], hi[i], o, inv, &entry) && entry <= w.t) {
-            const int slot = f2i(hi[i].w);
+        if (box_hit(r.lo[i], r.hi[i], o, inv, &entry) && entry <= w.t) {
+            const int slot = f2i(r.hi[i].w);
             if (slot >= 0) {
                 tri = slot;
                 return true;
             }
             w.pos++;
         } else {
-            w.pos = f2i(lo[i].w);
+            w.pos = f2i(r.lo[i].w);
             return false;
         }
     }
     return false;
+}
+template <int CHAIN>
+__device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri) {
+    ChainRecs<CHAIN> r;
+    chain_load<CHAIN>(rn, w.pos, r);
+    return chain_test<CHAIN>(r, o, inv, w, tri);
 }
 
 // walk_tri with the triangle's records already loaded.

@@ -1,0 +1,1 @@
+timeout -k 10 200 python tools/uprof.py
