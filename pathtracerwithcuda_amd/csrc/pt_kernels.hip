@@ -247,7 +247,6 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
     const int lane = threadIdx.x & 63;
     const LaunchParams* P0 = params;
     const float clamp_hi = (float)P0->cfg.max_depth * 2.0f;
-    const unsigned long long lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     // workgroup copies in LDS: the first mesh ranges and every material (the launch reserves
     // material_num * sizeof(DevMaterial) bytes of dynamic LDS; pass_kernel_u runs only when that fits)
     __shared__ int2 lds_mesh[PT_LDS_MESHES];
@@ -273,7 +272,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
     int32_t pseed = 0;
     int depth = 0;
     int mode = LANE_WANT;
-    unsigned long long segments = 0;
+    unsigned long long segments = 0;  // wave-uniform: lanes shaded (ray segments traced)
     Counters none = {0u, 0u, 0u, 0u, 0u, 0u};
     const unsigned int units = (unsigned int)P0->til.unit_count << batch_log2;
     const EvenRegions regions{units, (units + PT_SHARDS - 1) / PT_SHARDS};
@@ -281,7 +280,6 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
     bool drained = false;
     unsigned long long prof[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tc = 0;
-
     while (true) {
         const LaunchParams* P = params;
         asm volatile("" : "+s"(P));
@@ -298,7 +296,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
         const unsigned long long need_mask = __ballot(want);
         if (need_mask) {
             const unsigned int u = work_take(out.fetch, regions.stride, regions, (unsigned int)chunk, need_mask, want,
-                                             lane_lt, cursor, drained);
+                                             lanes_below(lane), cursor, drained);
             if (PROF) prof[7] += (unsigned long long)__popcll(__ballot(want && u != ~0u));
             if (want) {
                 if (u != ~0u) {
@@ -332,6 +330,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
         const unsigned long long walking = __ballot(mode == LANE_WALK || mode == LANE_TRI);
         if (ready && (__popcll(walking) <= (unsigned int)walk_min || __popcll(ready) >= (unsigned int)shade_min)) {
             if (PROF) { prof[3]++; prof[4] += (unsigned long long)__popcll(ready); }
+            segments += (unsigned long long)__popcll(ready);
             if (mode == LANE_READY) {
                 // the rest of trace_ray_kernel for this segment (:456-624)
                 if (PT_DUP == 1) {
@@ -342,7 +341,6 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                 }
                 const bool alive = shade_hit<false>(sc, cfg, depth, pseed, &ps, h, &none);
                 depth++;
-                segments++;
                 if (!alive || depth >= cfg.max_depth) {
                     finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
                     mode = LANE_WANT;
@@ -422,10 +420,8 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
         if (PROF) prof[10] += __builtin_readcyclecounter() - tc;
     }
 
-    unsigned long long s = segments;
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
     if (lane == 0) {
-        atomicAdd(&P0->out.stats[0], s);
+        atomicAdd(&P0->out.stats[0], segments);
         if (PROF) {
 #pragma unroll
             for (int k = 0; k < 11; k++) atomicAdd(&P0->out.stats[16 + k], prof[k]);
@@ -497,6 +493,7 @@ __global__ __launch_bounds__(PT_BLOCK) void math_eval_kernel(int which, const fl
         case 6: r0 = pow_pt(a, 1.85f); break;
         case 7: r0 = tan_pt(a); break;
         case 8: r0 = sqrtf(a); r1 = 1.0f / a; break;
+        case 9: r0 = u8_unit((unsigned int)a); break;  // texel byte -> [0, 1] (texture.h:47-66)
         default: break;
     }
     o0[i] = r0;
@@ -622,7 +619,8 @@ static PassFnU pass_fn_u(int minw, bool qn) {
     if (qn) return minw == 6 ? pass_kernel_u<6, false, true, 1, false> : pass_kernel_u<5, false, true, 1, false>;
     if (chain == 1) return minw == 6 ? pass_kernel_u<6, false, false, 1, false> : pass_kernel_u<5, false, false, 1, false>;
     if (chain == 3) return minw == 6 ? pass_kernel_u<6, false, false, 3, false> : pass_kernel_u<5, false, false, 3, false>;
-    if (pf) return minw == 6 ? pass_kernel_u<6, false, false, 2, true> : pass_kernel_u<5, false, false, 2, true>;
+    if (pf) return minw == 7 ? pass_kernel_u<7, false, false, 2, true>
+                             : (minw == 6 ? pass_kernel_u<6, false, false, 2, true> : pass_kernel_u<5, false, false, 2, true>);
     return minw == 6 ? pass_kernel_u<6, false, false, 2, false> : pass_kernel_u<5, false, false, 2, false>;
 }
 

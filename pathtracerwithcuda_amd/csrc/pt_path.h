@@ -173,20 +173,24 @@ __device__ __forceinline__ float fresnel_conductor(v3 n, v3 in, float eta, float
     return (rs + rp) / 2.0f;
 }
 
-// pixels[i] / 255.0f for i in 0..255 (texture.h:47-66). Tabulated: the quotients are the same
-// correctly rounded values (constant-folded), and no multiply by 1/255 reproduces all 256 of them.
-struct U8Quotients {
-    float v[256];
-    constexpr U8Quotients() : v() {
-        for (int i = 0; i < 256; i++) v[i] = (float)i / 255.0f;
-    }
-};
-__device__ __constant__ const U8Quotients kU8 = U8Quotients();
-
-__device__ __forceinline__ v3 texel(const uint8_t* px, int idx) {
-    uchar4 c = *reinterpret_cast<const uchar4*>(px + (size_t)idx * 4);
-    return mk3(kU8.v[c.x], kU8.v[c.y], kU8.v[c.z]);
+// pixels[i] / 255.0f (texture.h:47-66), exactly: the product with RN(1/255), corrected by one FMA step
+// with its exact residual. A plain multiply misses 126 of the 256 quotients; the corrected one
+// reproduces all 256 (test_u8_quotients_are_exact checks every value on the device).
+__device__ __forceinline__ float u8_unit(unsigned int b) {
+    const float f = (float)b;
+    const float c = 1.0f / 255.0f;
+    const float q = f * c;
+    const float r = fmaf(-q, 255.0f, f);
+    return fmaf(r, c, q);
 }
+
+// One RGBA8 texel as a packed word; channels are converted one at a time where they are used, so a
+// bilinear sample holds four words instead of twelve floats.
+__device__ __forceinline__ unsigned int texel_raw(const uint8_t* px, int idx) {
+    return *reinterpret_cast<const unsigned int*>(px + (size_t)idx * 4);
+}
+__device__ __forceinline__ float texel_c(unsigned int t, int c) { return u8_unit((t >> (8 * c)) & 0xffu); }
+__device__ __forceinline__ float lerp1(float a, float b, float t) { return a + t * (b - a); }
 
 // Core/texture.h:15-79 (also the face lookup of Core/cube_map.h:20-119, same arithmetic)
 __device__ __forceinline__ v3 sample_rgba8(const uint8_t* px, int w, int h, float au, float av, int bilinear) {
@@ -199,15 +203,18 @@ __device__ __forceinline__ v3 sample_rgba8(const uint8_t* px, int w, int h, floa
         int cy = (int)clampf(ceilf(yr), 0.0f, (float)(h - 1));
         float lr = xr - floorf(xr);
         float bt = yr - floorf(yr);
-        v3 c0 = texel(px, fy * w + fx);
-        v3 c1 = texel(px, fy * w + cx);
-        v3 c2 = texel(px, cy * w + fx);
-        v3 c3 = texel(px, cy * w + cx);
-        return lerp(lerp(c0, c1, lr), lerp(c2, c3, lr), bt);
+        const unsigned int t0 = texel_raw(px, fy * w + fx), t1 = texel_raw(px, fy * w + cx);
+        const unsigned int t2 = texel_raw(px, cy * w + fx), t3 = texel_raw(px, cy * w + cx);
+        float o[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++)  // lerp(lerp(c0, c1, lr), lerp(c2, c3, lr), bt), one channel at a time
+            o[c] = lerp1(lerp1(texel_c(t0, c), texel_c(t1, c), lr), lerp1(texel_c(t2, c), texel_c(t3, c), lr), bt);
+        return mk3(o[0], o[1], o[2]);
     }
     int x = (int)clampf(au * (float)(w - 1), 0.0f, (float)(w - 1));
     int y = (int)clampf((1.0f - av) * (float)(h - 1), 0.0f, (float)(h - 1));
-    return texel(px, y * w + x);
+    const unsigned int t = texel_raw(px, y * w + x);
+    return mk3(texel_c(t, 0), texel_c(t, 1), texel_c(t, 2));
 }
 
 __device__ __forceinline__ v3 sample_texture(const DevScene& sc, int id, v2 uv, int bilinear) {

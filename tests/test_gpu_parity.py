@@ -75,6 +75,15 @@ def test_device_math_matches_oracle_bitwise(gpu, which):
         assert same.all(), f"fn {which}: {(~same).sum()} mismatches, e.g. x={x[~same][:4]} gpu={a[~same][:4]} ref={b[~same][:4]}"
 
 
+def test_u8_quotients_are_exact(gpu):
+    """Texel bytes become pixels[i] / 255.0f (Core/texture.h:47-66); the device computes them with a
+    multiply and one FMA correction instead of a division or a table: all 256 must be the quotients."""
+    x = np.arange(256, dtype=np.float32)
+    d0, _ = gpu.math_eval_device(9, x)
+    want = x / np.float32(255.0)
+    assert np.array_equal(d0.view(np.uint32), want.view(np.uint32))
+
+
 def test_config1_spheres_only_cornell(gpu):
     sc = pt.cornell_spheres_scene(cube_length=64)
     cfg = pt.configuration(max_tracer_depth=4)
