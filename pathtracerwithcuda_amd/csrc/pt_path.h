@@ -672,11 +672,12 @@ __device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& 
 template <bool STATS>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
                                           PathState* ps, const Hit& h, Counters* ctr) {
-    const v3 o = ps->o, d = ps->d;
     const float min_t = h.t;
     minstd rng = minstd_seed(mul_wrap(pseed, hash_pt(depth)));
 
-    // medium: absorption and subsurface scattering (:456-492)
+    // medium: absorption and subsurface scattering (:456-492). A scattering lane replaces its ray in
+    // place, and the rest of the step reads the ray back from *ps afterwards (below), so the
+    // replaced and the original ray share registers instead of both living through the shading.
     {
         float sa[3], ss[3];
         medium_coefficients(sc, cfg, ps->medium, sa, ss);
@@ -686,7 +687,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
             if (dist < min_t) {
                 float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
                 float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
-                ps->o = o + d * dist;
+                ps->o = ps->o + ps->d * dist;
                 ps->d = sample_sphere(r1, r2);
                 ps->thr = ps->thr * absorption(sa, dist);
                 if (STATS) ctr->scatter++;
@@ -695,6 +696,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
             ps->thr = ps->thr * absorption(sa, min_t);
         }
     }
+    const v3 o = ps->o, d = ps->d;
 
     if (STATS) { ctr->miss += h.type == 0; ctr->hit_sphere += h.type == 1; ctr->hit_mesh += h.type == 2; }
     if (h.type == 0) {  // miss (:618-624)
@@ -703,12 +705,14 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
         return false;
     }
 
-    // material of the hit (:496-527); fields are read where they are used
+    // material of the hit (:496-527); fields are read where they are used. The texture modulation
+    // (:518-526) is applied in the branch that uses it (specular: reflect, diffuse: diffuse), from the
+    // interpolated uv, so only uv stays live through Fresnel and the bounce choice.
     const v3 point = o + d * min_t;
     v3 normal;
     int mid;
-    v3 tex_d = mk3(1.0f, 1.0f, 1.0f), tex_s = mk3(1.0f, 1.0f, 1.0f);
-    bool has_tex_d = false, has_tex_s = false;
+    v2 uv = mk2(0.0f, 0.0f);
+    bool textured = false;
     if (h.type == 1) {
         float4 s = sc.spheres[2 * h.prim];
         mid = f2i(sc.spheres[2 * h.prim + 1].x);
@@ -721,17 +725,14 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
         float w = 1.0f - h.t1 - h.t2;
         normal = n0 * w + n1 * h.t1 + n2 * h.t2;
         const DevMaterial& M = sc.materials[mid];
-        const int dt = M.diffuse_texture_id, st = M.specular_texture_id;
-        if (dt != -1 || st != -1) {
+        if (M.diffuse_texture_id != -1 || M.specular_texture_id != -1) {
             float4 s3 = sh[3];
             v2 uv0 = mk2(s2.y, s2.z), uv1 = mk2(s2.w, s3.x), uv2 = mk2(s3.y, s3.z);
-            v2 uv = uv0 * w + uv1 * h.t1 + uv2 * h.t2;
-            if (dt != -1) { tex_d = sample_texture(sc, dt, uv, cfg.use_bilinear); has_tex_d = true; }
-            if (st != -1) { tex_s = sample_texture(sc, st, uv, cfg.use_bilinear); has_tex_s = true; }
+            uv = uv0 * w + uv1 * h.t1 + uv2 * h.t2;
+            textured = true;
         }
     }
     const DevMaterial& M = sc.materials[mid];
-
     // media on either side of the surface (:529-547)
     float in_n = cfg.air_n;
     float out_n = M.refraction_index;
@@ -774,13 +775,15 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
             v3 mr = reflection(dir, d);
             float shadow = ggx_g1(rough, normal, dir, d) * ggx_g1(rough, normal, dir, mr);
             v3 spec = mk3(M.specular[0], M.specular[1], M.specular[2]);
-            if (has_tex_s) spec = spec * tex_s;
+            if (textured && M.specular_texture_id != -1)
+                spec = spec * sample_texture(sc, M.specular_texture_id, uv, cfg.use_bilinear);
             ps->o = point + bias_v;
             ps->d = mr;
             ps->thr = ps->thr * (spec * shadow);
         } else {        // diffuse (:597-610)
             v3 diff = mk3(M.diffuse[0], M.diffuse[1], M.diffuse[2]);
-            if (has_tex_d) diff = diff * tex_d;
+            if (textured && M.diffuse_texture_id != -1)
+                diff = diff * sample_texture(sc, M.diffuse_texture_id, uv, cfg.use_bilinear);
             ps->rad = ps->rad + ps->thr * mk3(M.emission[0], M.emission[1], M.emission[2]);
             ps->thr = ps->thr * diff;
             ps->o = point + bias_v;
