@@ -213,9 +213,12 @@ __device__ __forceinline__ int begin_segment(const DevScene& sc, const int2* lds
             h.t = t; h.prim = i; h.type = 1;
         }
     }
-    mesh = 0;
-    if (sc.mesh_num > 0) inv = 1.0f / ps.d;
-    return start_mesh(sc, lds_mesh, mesh, w) ? LANE_WALK : LANE_READY;
+    if (sc.first_mesh >= sc.mesh_num) return LANE_READY;  // (start_mesh from mesh 0, resolved on the host)
+    inv = 1.0f / ps.d;
+    mesh = sc.first_mesh;
+    w.pos = sc.first_range.x; w.end = sc.first_range.y;
+    w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
+    return LANE_WALK;
 }
 
 // pixel_256_transform_gamma_corrected_kernel (:644-680) for one finished (pixel, pass) unit
@@ -247,8 +250,8 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
     const int lane = threadIdx.x & 63;
     const LaunchParams* P0 = params;
     const float clamp_hi = (float)P0->cfg.max_depth * 2.0f;
-    // workgroup copies in LDS: the first mesh ranges and every material (the launch reserves
-    // material_num * sizeof(DevMaterial) bytes of dynamic LDS; pass_kernel_u runs only when that fits)
+    // workgroup copies in LDS: the first mesh ranges, every material and every sphere (the launch
+    // reserves their bytes of dynamic LDS; pass_kernel_u runs only when that fits, PT_LDS_TABLES)
     __shared__ int2 lds_mesh[PT_LDS_MESHES];
     extern __shared__ float4 lds_dyn[];
     DevMaterial* lds_mats = reinterpret_cast<DevMaterial*>(lds_dyn);
@@ -259,8 +262,12 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
         const float4* ms = reinterpret_cast<const float4*>(uniform_ptr(P0->sc.materials));
         const int nm = uniform_int(P0->sc.material_num) * (int)(sizeof(DevMaterial) / 16);
         for (int i = threadIdx.x; i < nm; i += PT_BLOCK) lds_dyn[i] = ms[i];
+        const float4* sp = uniform_ptr(P0->sc.spheres);
+        const int ns = uniform_int(P0->sc.sphere_num) * 2;
+        for (int i = threadIdx.x; i < ns; i += PT_BLOCK) lds_dyn[nm + i] = sp[i];
         __syncthreads();
     }
+    const float4* lds_spheres = lds_dyn + uniform_int(P0->sc.material_num) * (int)(sizeof(DevMaterial) / 16);
 
     PathState ps;
     v3 inv = mk3(0.0f, 0.0f, 0.0f);
@@ -278,14 +285,15 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
     const EvenRegions regions{units, (units + PT_SHARDS - 1) / PT_SHARDS};
     WorkCursor cursor = work_begin();
     bool drained = false;
-    unsigned long long prof[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long tc = 0;
+    unsigned long long prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tc = 0, tc2 = 0;
     while (true) {
         const LaunchParams* P = params;
         asm volatile("" : "+s"(P));
         P = uniform_ptr(P);
         DevScene sc = load_const(&P->sc);
         sc.materials = lds_mats;
+        sc.spheres = lds_spheres;
         const DevConfig cfg = load_const(&P->cfg);
         const DevTiling til = load_const(&P->til);
         const DevOutput out = load_const(&P->out);
@@ -331,6 +339,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
         if (ready && (__popcll(walking) <= (unsigned int)walk_min || __popcll(ready) >= (unsigned int)shade_min)) {
             if (PROF) { prof[3]++; prof[4] += (unsigned long long)__popcll(ready); }
             segments += (unsigned long long)__popcll(ready);
+            bool alive = false;
             if (mode == LANE_READY) {
                 // the rest of trace_ray_kernel for this segment (:456-624)
                 if (PT_DUP == 1) {
@@ -339,7 +348,10 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                     bool a2 = shade_hit<false>(sc, cfg, d2, pseed, &p2, h2, &none);
                     opaque(p2); opaque(a2);
                 }
-                const bool alive = shade_hit<false>(sc, cfg, depth, pseed, &ps, h, &none);
+                alive = shade_hit<false>(sc, cfg, depth, pseed, &ps, h, &none, PROF ? prof + 11 : nullptr);
+            }
+            if (PROF) tc2 = __builtin_readcyclecounter();
+            if (mode == LANE_READY) {  // the pass's end for this unit, or the next trace step
                 depth++;
                 if (!alive || depth >= cfg.max_depth) {
                     finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
@@ -348,6 +360,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
                     mode = begin_segment(sc, lds_mesh, ps, inv, h, w, mesh);
                 }
             }
+            if (PROF) prof[15] += __builtin_readcyclecounter() - tc2;
             if (PROF) prof[9] += __builtin_readcyclecounter() - tc;
             continue;
         }
@@ -424,7 +437,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
         atomicAdd(&P0->out.stats[0], segments);
         if (PROF) {
 #pragma unroll
-            for (int k = 0; k < 11; k++) atomicAdd(&P0->out.stats[16 + k], prof[k]);
+            for (int k = 0; k < 16; k++) atomicAdd(&P0->out.stats[16 + k], prof[k]);
         }
     }
 }
@@ -624,16 +637,17 @@ static PassFnU pass_fn_u(int minw, bool qn) {
     return minw == 6 ? pass_kernel_u<6, false, false, 2, false> : pass_kernel_u<5, false, false, 2, false>;
 }
 
-// pass_kernel_u keeps every material in LDS: scenes with more than PT_LDS_MATERIALS run pass_kernel.
-#define PT_LDS_MATERIALS 256
-static bool use_unified(bool leaf1, bool stats, bool qn, int material_num) {
+// pass_kernel_u keeps every material and sphere in LDS: scenes whose tables exceed PT_LDS_TABLES bytes
+// (about 256 materials and 256 spheres) run pass_kernel.
+#define PT_LDS_TABLES (32 * 1024)
+static bool use_unified(bool leaf1, bool stats, bool qn, int lds_bytes) {
     (void)qn;
-    return leaf1 && !stats && unified_enabled() && material_num <= PT_LDS_MATERIALS;
+    return leaf1 && !stats && unified_enabled() && lds_bytes <= PT_LDS_TABLES;
 }
 
 hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int first_pass, int batch_log2,
-                       int write_u8, int grid, bool stats, int material_num, hipStream_t stream) {
-    if (use_unified(leaf1, stats, qn, material_num)) {
+                       int write_u8, int grid, bool stats, int lds_bytes, hipStream_t stream) {
+    if (use_unified(leaf1, stats, qn, lds_bytes)) {
         static const int chunk = env_int("PT_CHUNK_MEGA", 32, 0, 4096);
         static const int shade_min = env_int("PT_SHADE_MIN", 32, 1, 64);
         static const int walk_steps = env_int("PT_WALK_STEPS", 10, 1, 64);
@@ -644,7 +658,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int 
             a8 = walk_min;
         void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8};
         hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn), dim3(grid), dim3(PT_BLOCK), args,
-                                       (size_t)material_num * sizeof(DevMaterial), stream);
+                                       (size_t)lds_bytes, stream);
         if (e != hipSuccess) return e;
         return hipGetLastError();
     }
@@ -674,14 +688,14 @@ hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256
     return hipGetLastError();
 }
 
-int pass_grid_size(bool leaf1, bool stats, bool qn, int material_num) {
+int pass_grid_size(bool leaf1, bool stats, bool qn, int lds_bytes) {
     int dev = 0, cus = 0, blocks = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const bool u = use_unified(leaf1, stats, qn, material_num);
+    const bool u = use_unified(leaf1, stats, qn, lds_bytes);
     const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true), qn)
                        : (const void*)pass_fn(leaf1, stats, pass_min_waves(false), qn);
-    const size_t lds = u ? (size_t)material_num * sizeof(DevMaterial) : 0;
+    const size_t lds = u ? (size_t)lds_bytes : 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, PT_BLOCK, lds) != hipSuccess || blocks <= 0) blocks = 4;
     if (cus <= 0) cus = 256;
     return cus * blocks;

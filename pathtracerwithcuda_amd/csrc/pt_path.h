@@ -655,7 +655,7 @@ __device__ __forceinline__ int32_t path_seed(int32_t hseed, int pixel) { return 
 
 template <bool STATS>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
-                                          PathState* ps, const Hit& h, Counters* ctr);
+                                          PathState* ps, const Hit& h, Counters* ctr, unsigned long long* pc = nullptr);
 
 // One invocation of trace_ray_kernel for one live ray (path_tracer_kernel.cu:381-625).
 // pseed = path_seed(hash(pass), pixel). Returns false when the reference would write -1 into
@@ -669,9 +669,15 @@ __device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& 
 
 // The part of trace_ray_kernel after the closest hit is known (:456-624): medium, material,
 // Fresnel-selected bounce, accumulation, kill test.
+// pc (PT_UPROF builds): cycles spent per phase, added into pc[0..3] (medium, hit record or miss,
+// Fresnel, bounce).
 template <bool STATS>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
-                                          PathState* ps, const Hit& h, Counters* ctr) {
+                                          PathState* ps, const Hit& h, Counters* ctr, unsigned long long* pc) {
+    unsigned long long tq = pc ? __builtin_readcyclecounter() : 0;
+    auto mark = [&](int i) {
+        if (pc) { const unsigned long long t = __builtin_readcyclecounter(); pc[i] += t - tq; tq = t; }
+    };
     const float min_t = h.t;
     minstd rng = minstd_seed(mul_wrap(pseed, hash_pt(depth)));
 
@@ -696,6 +702,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
             ps->thr = ps->thr * absorption(sa, min_t);
         }
     }
+    mark(0);
     const v3 o = ps->o, d = ps->d;
 
     if (STATS) { ctr->miss += h.type == 0; ctr->hit_sphere += h.type == 1; ctr->hit_mesh += h.type == 2; }
@@ -733,6 +740,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
         }
     }
     const DevMaterial& M = sc.materials[mid];
+    mark(1);
     // media on either side of the surface (:529-547)
     float in_n = cfg.air_n;
     float out_n = M.refraction_index;
@@ -753,6 +761,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
     if (k == 0 || transparent) R = fresnel_dielectric(normal, d, in_n, out_n, refr, out_medium < 0 ? M.tir_back : M.tir_front);
     else R = fresnel_conductor(normal, d, out_n, k);
 
+    mark(2);
     // Bounce (:563-610). The reflect and diffuse branches both draw r1, r2 right after r and build
     // their direction with the same hemisphere tail, so the draws and the tail are shared (a refract
     // lane draws them too and ignores them: the generator is local to this step).
@@ -796,6 +805,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
         float ratio = out_n / in_n;
         ps->thr = ps->thr * (ratio * ratio);
     }
+    mark(3);
     return length(ps->thr) > cfg.energy_threshold;
 }
 

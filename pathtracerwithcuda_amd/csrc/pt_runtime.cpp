@@ -415,6 +415,14 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     s.node_count = (int)(st.nodes.size() / 2);
     s.tri_count = (int)(st.tri_geom.size() / 3);
     s.material_num = (int)st.mats.size();
+    s.first_mesh = (int)st.mesh_range.size();
+    s.first_range = int2{0, 0};
+    for (size_t m = 0; m < st.mesh_range.size(); m++)
+        if (st.mesh_range[m].x != st.mesh_range[m].y) {
+            s.first_mesh = (int)m;
+            s.first_range = st.mesh_range[m];
+            break;
+        }
     ctx->node_num = (int)(st.nodes.size() / 2);
     ctx->tri_num = (int)(st.tri_geom.size() / 3);
     ctx->material_num = (int)st.mats.size();
@@ -477,10 +485,15 @@ bool use_qnodes(const pt_context* ctx) {
     return on && ctx->scene.qnodes != nullptr;
 }
 
+// dynamic LDS of pass_kernel_u: every material, then every sphere record (pt_kernels.hip)
+int pass_lds_bytes(const pt_context* ctx) {
+    return ctx->material_num * (int)sizeof(DevMaterial) + ctx->scene.sphere_num * 32;
+}
+
 int pass_grid(pt_context* ctx) {
     const bool leaf1 = ctx->scene.leaf_size == 1, qn = use_qnodes(ctx);
     int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0][qn ? 1 : 0];
-    if (g == 0) g = pass_grid_size(leaf1, ctx->instrumented, qn, ctx->material_num);
+    if (g == 0) g = pass_grid_size(leaf1, ctx->instrumented, qn, pass_lds_bytes(ctx));
     return g;
 }
 
@@ -647,7 +660,7 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         int rc = ev_begin(ctx, 0);
         if (rc != PT_OK) return rc;
         PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, use_qnodes(ctx), first, lg, w8, grid,
-                           ctx->instrumented, ctx->material_num, ctx->stream));
+                           ctx->instrumented, pass_lds_bytes(ctx), ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         if (lg > 0) {
             if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;

@@ -76,6 +76,8 @@ struct DevScene {
     int node_count;  // records in `nodes` (2 float4 each); bounds of the node buffer descriptor
     int tri_count;   // records in `tri_geom` (3 float4 each)
     int material_num;  // records in `materials`
+    int first_mesh;    // first mesh with a non-empty node range (mesh_num if none) and that range:
+    int2 first_range;  //   where every trace step's mesh walk starts
 };
 
 // The subset of Core/configuration.h:9-34 that the kernel reads.

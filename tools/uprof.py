@@ -25,7 +25,8 @@ buf = (C.c_ulonglong * 32)()
 pt.lib().pt_stats_all(r._ctx, buf, 32)
 v = list(buf)
 names = ["rounds", "walk_steps", "walking_lanes", "shade_batches", "lanes_shaded", "tri_batches", "tri_lanes", "refilled",
-         "cyc_refill", "cyc_shade", "cyc_walk"]
+         "cyc_refill", "cyc_shade", "cyc_walk", "shade_cyc_medium", "shade_cyc_hit_or_miss", "shade_cyc_fresnel",
+         "shade_cyc_bounce", "shade_cyc_next_segment"]
 d = {n: v[16 + i] for i, n in enumerate(names)}
 d["segments"] = v[0]
 d["lanes_per_walk_step"] = round(d["walking_lanes"] / max(d["walk_steps"], 1), 2)
@@ -37,4 +38,6 @@ for k in ("cyc_refill", "cyc_shade", "cyc_walk"):
     d[k.replace("cyc", "frac")] = round(d[k] / max(tot, 1), 3)
 d["cyc_per_walk_round"] = round(d["cyc_walk"] / max(d["rounds"] - d["shade_batches"], 1))
 d["cyc_per_shade_batch"] = round(d["cyc_shade"] / max(d["shade_batches"], 1))
+for k in ("shade_cyc_medium", "shade_cyc_hit_or_miss", "shade_cyc_fresnel", "shade_cyc_bounce", "shade_cyc_next_segment"):
+    d[k.replace("shade_cyc", "shade_frac")] = round(d[k] / max(d["cyc_shade"], 1), 3)
 print(json.dumps(d))
