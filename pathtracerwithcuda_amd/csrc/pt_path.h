@@ -465,6 +465,11 @@ __device__ __forceinline__ void chain_load(const __amdgpu_buffer_rsrc_t rn, int 
         r.lo[i] = bload(rn, (pos + i) * 32);
         r.hi[i] = bload(rn, (pos + i) * 32 + 16);
     }
+    // Left alone, the compiler sinks the later records' loads into the branch that tests them, which
+    // makes them a second dependent round trip. Using them here keeps all loads of the step issued
+    // together (one round trip).
+#pragma unroll
+    for (int i = 1; i < CHAIN; i++) asm volatile("" ::"v"(r.lo[i].w), "v"(r.hi[i].w));
 }
 template <int CHAIN>
 __device__ __forceinline__ bool chain_test(const ChainRecs<CHAIN>& r, v3 o, v3 inv, MeshWalk& w, int& tri) {
