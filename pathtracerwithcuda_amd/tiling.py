@@ -57,6 +57,11 @@ class TiledFrame:
 
     def render(self, cam, cfg, spp: int) -> None:
         """Passes 1..spp; rank 0 ends with the full float image and its 8-bit output."""
+        if self.world > 1:
+            # rows outside this rank's bands must be zero for the reduce, and rank 0's buffer still
+            # holds the previous frame's sum: clear it (the renderer runs on its own stream: sync)
+            self.image.zero_()
+            self._device_sync()
         self.r.render(cam, cfg, 1, spp, write_u8=2 if self.world == 1 else 0)
         if self.world > 1:
             self.r.synchronize()

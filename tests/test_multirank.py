@@ -74,7 +74,8 @@ def _worker(rank, world, port, out_dir):
         r = OracleFrameRenderer(scene)
         frame = pt.TiledFrame(r, W, H, dist, BAND, device="cpu")
         assert frame.world == world and frame.rank == rank
-        frame.render(cam, cfg, SPP)
+        for _ in range(2):  # a second frame must not see the first one's reduced sum (bench renders many)
+            frame.render(cam, cfg, SPP)
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), img=r.img.copy(), img8=r.img8.copy(),
                  owned=pt.owned_pixels(W, H, BAND, world, rank))
     finally:

@@ -1,2 +1,1 @@
-mkdir -p gpurun_out/sq2
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/sq2/a -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/sq2/a.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sq2/b -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/sq2/b.log 2>&1 && python3 tools/pmc_summary.py gpurun_out/sq2
+PT_LIBDIR=$GRAFT_REPO_ROOT/pathtracerwithcuda_amd/lib_seg timeout -k 10 200 python tools/uprof.py
