@@ -214,7 +214,7 @@ __device__ __forceinline__ int begin_segment(const DevScene& sc, const int2* lds
         }
     }
     if (sc.first_mesh >= sc.mesh_num) return LANE_READY;  // (start_mesh from mesh 0, resolved on the host)
-    inv = 1.0f / ps.d;
+    inv = mk3(rcp_exact(ps.d.x), rcp_exact(ps.d.y), rcp_exact(ps.d.z));  // == 1.0f / d
     mesh = sc.first_mesh;
     w.pos = sc.first_range.x; w.end = sc.first_range.y;
     w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
@@ -507,6 +507,7 @@ __global__ __launch_bounds__(PT_BLOCK) void math_eval_kernel(int which, const fl
         case 7: r0 = tan_pt(a); break;
         case 8: r0 = sqrtf(a); r1 = 1.0f / a; break;
         case 9: r0 = u8_unit((unsigned int)a); break;  // texel byte -> [0, 1] (texture.h:47-66)
+        case 10: r0 = rcp_exact(a); r1 = 1.0f / a; break;
         default: break;
     }
     o0[i] = r0;

@@ -84,6 +84,19 @@ def test_u8_quotients_are_exact(gpu):
     assert np.array_equal(d0.view(np.uint32), want.view(np.uint32))
 
 
+def test_rcp_exact_matches_division(gpu):
+    """rcp_exact (v_rcp_f32 + one Newton step) against the IEEE division 1.0f / x on the device: every
+    significand in [1, 2) at several exponents and both signs, plus the guarded edges."""
+    sig = (np.arange(1 << 23, dtype=np.uint32) | np.uint32(127 << 23)).view(np.float32)
+    xs = [sig, -sig, sig * np.float32(2.0 ** -120), sig * np.float32(2.0 ** 100), sig * np.float32(2.0 ** -30)]
+    xs.append(np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-40, -1e-40, 2.0 ** -125, 2.0 ** 125, 2.0 ** -126,
+                        3.4e38, 1.2e-38], np.float32))
+    x = np.concatenate(xs).astype(np.float32)
+    fast, div = gpu.math_eval_device(10, x)
+    same = (fast.view(np.uint32) == div.view(np.uint32)) | (np.isnan(fast) & np.isnan(div))
+    assert same.all(), f"{(~same).sum()} mismatches, e.g. x={x[~same][:4]} fast={fast[~same][:4]} div={div[~same][:4]}"
+
+
 def test_config1_spheres_only_cornell(gpu):
     sc = pt.cornell_spheres_scene(cube_length=64)
     cfg = pt.configuration(max_tracer_depth=4)
