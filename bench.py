@@ -51,6 +51,86 @@ def extend_bytes(counts: dict, sphere_count: int) -> float:
     return (24.0 + 16.0 + 16.0 * sphere_count) * seg + 32.0 * counts["nodes"] + 40.0 * counts["tris"]
 
 
+def procedural_texture(w: int, h: int, seed: int) -> np.ndarray:
+    """RGBA8 texture (top row first): checker tiles with per-tile colour noise."""
+    rng = np.random.default_rng(seed)
+    tiles = rng.integers(40, 255, (8, 8, 3))
+    y, x = np.mgrid[0:h, 0:w]
+    c = tiles[(y * 8 // h) % 8, (x * 8 // w) % 8]
+    img = np.concatenate([c, np.full((h, w, 1), 255)], -1)
+    img[..., :3] = (img[..., :3] * (0.75 + 0.25 * ((x // 16 + y // 16) % 2))[..., None]).astype(np.int64)
+    return img.astype(np.uint8)
+
+
+class Workload:
+    """One benchmark workload: scene, configuration, camera and frame size. `metric` is the configuration
+    BASELINE.json's metric is quoted on (the default line); c3-c5 are the heavier BASELINE.json configs
+    (1 GPU or tiled), for one-off measurements of the same path at their sizes."""
+
+    def __init__(self, name: str):
+        import pathtracerwithcuda_amd as pt
+
+        self.name = name
+        cam_kw = dict(CAMERA)
+        if name == "metric":
+            self.width, self.height, self.spp, self.depth = WIDTH, HEIGHT, SPP, DEPTH
+            self.scene = pt.cornell_scene(pt.torus_knot(*KNOT))
+            self.key = f"cornell+knot{KNOT[0] * KNOT[1] * 2}_{WIDTH}x{HEIGHT}_spp{SPP}_d{DEPTH}"
+            self.desc = ("Cornell box (cornell.obj walls, cube.obj light, iron+glass spheres) + torus knot, "
+                         f"{self.scene.triangle_count} triangles, {self.scene.view.sphere_num} spheres")
+            self.data = "synthetic: procedural 70k-triangle torus knot (bunny stand-in) + procedural 512^2 cube map"
+        elif name == "c3":  # micro_surface.json: six GGX spheres, skybox, depth of field
+            self.width, self.height, self.spp, self.depth = 1920, 1080, 64, 8
+            sc = pt.Scene()
+            for i, x in enumerate(np.linspace(-2.5, 2.5, 6)):
+                sc.add_sphere((float(x), 0.4, 0.0), 0.45, f"Micro{i + 1}")
+            walls = [sc.add_material(m) for m in ("wall_white", "wall_green", "wall_red", "wall_white", "wall_white")]
+            sc.add_mesh(pt.cornell_shapes(), walls, position=(0.0, -0.8, 1.0), scale=(0.1, 0.1, 0.3))
+            sc.add_mesh([pt.cube_shape()], [sc.add_material("light")], position=(0.0, 3.1, 0.0),
+                        scale=(0.85, 0.05, 0.85))
+            sc.set_cube_map(pt.procedural_cube_map(512))
+            self.scene = sc.build()
+            cam_kw.update(aperture=0.1, focal=12.5)
+            self.key = "c3_microfacet_sky_dof_1920x1080_spp64_d8"
+            self.desc = "six GGX spheres (roughness 0.01..1, silver n=0.04 k=2.65), Cornell walls + light, skybox, DoF 0.1"
+            self.data = "synthetic: micro_surface.json spheres + procedural 512^2 cube map"
+        elif name == "c4":  # ~800k-triangle mesh with the dragon's subsurface material
+            self.width, self.height, self.spp, self.depth = 1920, 1080, 256, 8
+            self.scene = pt.cornell_scene(pt.torus_knot(1000, 400), mesh_material="DragonGreen")
+            self.key = "c4_knot800000_sss_1920x1080_spp256_d8"
+            self.desc = (f"Cornell box + {self.scene.triangle_count - 22}-triangle torus knot (dragon stand-in) "
+                         "with DragonGreen subsurface scattering (sigma_a (40,3,14), sigma_s' 400)")
+            self.data = "synthetic: procedural 800k-triangle torus knot + procedural 512^2 cube map"
+        elif name == "c5":  # multi-mesh, diffuse + specular texture maps, 4K
+            self.width, self.height, self.spp, self.depth = 3840, 2160, 1024, 12
+            sc = pt.Scene()
+            walls = [sc.add_material(m) for m in ("wall_white", "wall_green", "wall_red", "wall_white", "wall_white")]
+            sc.add_mesh(pt.cornell_shapes(), walls, position=(0.0, -0.8, 1.0), scale=(0.1, 0.1, 0.3))
+            sc.add_mesh([pt.cube_shape()], [sc.add_material("light")], position=(0.0, 3.1, 0.0),
+                        scale=(0.85, 0.05, 0.85))
+            for k, (pos, rot, base) in enumerate([((-1.3, 0.6, -0.8), (0, 30, 0), "red"),
+                                                  ((1.2, 0.6, -0.6), (20, -20, 0), "green"),
+                                                  ((0.0, 1.9, -1.6), (70, 0, 0), "gold")]):
+                td = sc.add_texture(procedural_texture(512, 256, 10 + k))
+                ts = sc.add_texture(procedural_texture(256, 256, 20 + k))
+                m = sc.add_material(pt.material(base, diffuse_texture_id=td, specular_texture_id=ts))
+                sc.add_mesh([pt.torus_knot(300, 60, uv_repeat=6.0)], [m], position=pos, scale=(0.45, 0.45, 0.45),
+                            rotate=rot)
+            tc = sc.add_texture(procedural_texture(1024, 1024, 30))
+            mc = sc.add_material(pt.material("diffuse_white", diffuse_texture_id=tc, specular_texture_id=tc))
+            sc.add_mesh([pt.cube_shape()], [mc], position=(0.0, 0.0, 0.6), scale=(0.6, 0.6, 0.6), rotate=(0, 35, 0))
+            sc.set_cube_map(pt.procedural_cube_map(512))
+            self.scene = sc.build()
+            self.key = "c5_textured_multimesh_3840x2160_spp1024_d12"
+            self.desc = (f"Cornell box + three textured torus knots + a textured cube, {self.scene.triangle_count} "
+                         "triangles, diffuse and specular RGBA8 maps")
+            self.data = "synthetic: procedural meshes and textures + procedural 512^2 cube map"
+        else:
+            raise SystemExit(f"unknown workload {name!r}")
+        self.cfg = pt.configuration(max_tracer_depth=self.depth)
+        self.cam = pt.camera(self.width, self.height, **cam_kw)
+
+
 def cpu_baseline(scene, cam, cfg, threads: int) -> dict:
     """The reference's CPU fallback semantics (Core/path_tracer_cpu.cpp: MSVC rand, libm), as
     restated by the oracle, on the same frame: one whole frame (all 8 passes), so ms/frame is measured,
@@ -90,6 +170,8 @@ def main() -> int:
     ap.add_argument("--save-image", default="")
     ap.add_argument("--schedule", choices=["persistent", "wavefront"], default=None,
                     help="kernel schedule (default: the library's, PT_MODE)")
+    ap.add_argument("--workload", choices=["metric", "c3", "c4", "c5"], default="metric",
+                    help="metric: BASELINE.json's metric configuration (default); c3-c5: its heavier configs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -112,20 +194,20 @@ def main() -> int:
     r = pt.Renderer(local)
     r.set_schedule(args.schedule)
     schedule = r.schedule()
-    scene = pt.cornell_scene(pt.torus_knot(*KNOT))
-    cfg = pt.configuration(max_tracer_depth=DEPTH)
-    cam = pt.camera(WIDTH, HEIGHT, **CAMERA)
+    wl = Workload(args.workload)
+    scene, cfg, cam = wl.scene, wl.cfg, wl.cam
+    width, height, spp = wl.width, wl.height, wl.spp
     r.upload(scene, cfg)
-    tiled = pt.TiledFrame(r, WIDTH, HEIGHT, dist if world > 1 else None, BAND_ROWS,
+    tiled = pt.TiledFrame(r, width, height, dist if world > 1 else None, BAND_ROWS,
                           device=f"cuda:{local}" if world > 1 else None)
 
     def frame():
-        tiled.render(cam, cfg, SPP)
+        tiled.render(cam, cfg, spp)
 
     # roofline inputs: one instrumented (untimed) frame for the visit counts
     r.set_instrumented(True)
     r.stats_reset()
-    r.render(cam, cfg, 1, SPP, write_u8=0)
+    r.render(cam, cfg, 1, spp, write_u8=0)
     r.synchronize()
     counts = r.stats_all()
     r.set_instrumented(False)
@@ -175,7 +257,7 @@ def main() -> int:
     if schedule == "persistent":
         # one launch = a batch of passes over the frame (this rank's bands when tiled)
         bytes_per_launch = algorithmic_bytes(counts, scene.view.sphere_num, cfg.bvh_leaf_node_triangle_num,
-                                             WIDTH * HEIGHT, SPP) / world / launches_per_frame
+                                             width * height, spp) / world / launches_per_frame
         kernel_name = (f"pass_kernel_u<MINW={os.environ.get('PT_MIN_WAVES', '6')},"
                        f"CHAIN={os.environ.get('PT_WALK_CHAIN', '2')},PF={os.environ.get('PT_TRI_PREFETCH', '1')}>"
                        if os.environ.get("PT_UNIFIED", "1") != "0" else "pass_kernel<LEAF1=true,STATS=false,MINW=8>")
@@ -184,7 +266,7 @@ def main() -> int:
         bytes_per_launch = extend_bytes(counts, scene.view.sphere_num) / world / launches_per_frame
         kernel_name = "extend_kernel<LEAF1=true,STATS=false>"
     achieved = bytes_per_launch / avg_launch_s / 1e9
-    workload = f"cornell+knot{KNOT[0] * KNOT[1] * 2}_{WIDTH}x{HEIGHT}_spp{SPP}_d{DEPTH}"
+    workload = wl.key
     traffic = load_traffic(workload + ("" if schedule == "persistent" else "/wavefront"))
     line = {
         "metric": "Mrays/sec + ms/frame @1920x1080, 8spp, 8-bounce; 1/2/4/8 GPU",
@@ -198,17 +280,16 @@ def main() -> int:
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: procedural 70k-triangle torus knot (bunny stand-in) + procedural 512^2 cube map",
+        "data": wl.data,
         "config": {
             "workload": workload,
-            "scene": "Cornell box (cornell.obj walls, cube.obj light, iron+glass spheres) + torus knot, "
-                     f"{scene.triangle_count} triangles, {scene.view.sphere_num} spheres",
-            "width": WIDTH, "height": HEIGHT, "spp": SPP, "max_depth": DEPTH,
+            "scene": wl.desc,
+            "width": width, "height": height, "spp": spp, "max_depth": wl.depth,
             "parallelism": f"tiled{world}" if world > 1 else "single",
             "schedule": schedule,
             "band_rows": BAND_ROWS if world > 1 else None,
             "ms_per_frame": round(ms_per_step, 3),
-            "camera_samples_per_s_M": round(WIDTH * HEIGHT * SPP * args.steps / elapsed / 1e6, 3),
+            "camera_samples_per_s_M": round(width * height * spp * args.steps / elapsed / 1e6, 3),
             "segments_per_frame": segments // max(args.steps, 1),
         },
         "roofline": {
@@ -226,7 +307,7 @@ def main() -> int:
         },
         "cpu_baseline": None,
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and args.workload == "metric":
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(scene, cam, cfg, threads)
         line["cpu_baseline"]["cpu"] = platform.processor() or platform.machine()

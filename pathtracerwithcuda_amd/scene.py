@@ -130,7 +130,7 @@ def cube_shape() -> Shape:
 
 
 def torus_knot(tubular: int = 350, radial: int = 100, p: int = 2, q: int = 3, radius: float = 1.0,
-               tube: float = 0.3) -> Shape:
+               tube: float = 0.3, uv_repeat: float = 0.0) -> Shape:
     """Procedural (p,q) torus knot with 2*tubular*radial triangles and analytic tube normals.
 
     Stands in for the ~70k-triangle Stanford bunny of config 2 (350x100x2 = 70,000) and, at
@@ -165,7 +165,16 @@ def torus_knot(tubular: int = 350, radial: int = 100, p: int = 2, q: int = 3, ra
     idx = [(a, b, d), (b, c, d)]
     V = np.concatenate([np.stack([pos[x] for x in tri], axis=2).reshape(-1, 3, 3) for tri in idx])
     Nr = np.concatenate([np.stack([nrm[x] for x in tri], axis=2).reshape(-1, 3, 3) for tri in idx])
-    return Shape(V.astype(np.float32), Nr.astype(np.float32))
+    uvs = None
+    if uv_repeat > 0:  # texture coordinates along (u: the knot, v: around the tube), `uv_repeat` tiles per loop
+        tu = np.broadcast_to((np.arange(tubular + 1)[:, None] / tubular * uv_repeat), (tubular + 1, radial + 1))
+        tv = np.broadcast_to((np.arange(radial + 1)[None, :] / radial), (tubular + 1, radial + 1))
+        tex = np.stack([tu, tv], -1)
+        ii, jj = np.arange(tubular)[:, None], np.arange(radial)[None, :]
+        ta, tb, tc, td = (ii, jj), (ii + 1, jj), (ii + 1, jj + 1), (ii, jj + 1)  # unwrapped (no modulo)
+        uvs = np.concatenate([np.stack([tex[x] for x in tri], axis=2).reshape(-1, 3, 2)
+                              for tri in [(ta, tb, td), (tb, tc, td)]]).astype(np.float32)
+    return Shape(V.astype(np.float32), Nr.astype(np.float32), uvs)
 
 
 def procedural_cube_map(length: int = 512, seed: int = 7) -> np.ndarray:
