@@ -452,10 +452,20 @@ __global__ __launch_bounds__(PT_BLOCK) void accumulate_kernel(const LaunchParams
     const int batch = 1 << batch_log2;
     float* img = P->out.image + (size_t)pixel * 3;
     const float* pr = P->out.pass_rad + ((size_t)lu << batch_log2) * 3;
-    v3 sum = mk3(img[0], img[1], img[2]);
-    for (int j = 0; j < batch; j++) {
-        const v3 c = mk3(pr[3 * j], pr[3 * j + 1], pr[3 * j + 2]);
-        sum = (first_pass + j == 1) ? c : sum + c;
+    v3 sum = first_pass == 1 ? mk3(0.0f, 0.0f, 0.0f) : mk3(img[0], img[1], img[2]);  // pass 1 overwrites
+    if ((batch & 3) == 0) {  // four passes = 12 floats = three 16-B loads (the unit's run is 16-B aligned)
+        const float4* q = reinterpret_cast<const float4*>(pr);
+        for (int g = 0; g < batch / 4; g++) {
+            const float4 a = q[3 * g], b = q[3 * g + 1], c = q[3 * g + 2];
+            const v3 cs[4] = {mk3(a.x, a.y, a.z), mk3(a.w, b.x, b.y), mk3(b.z, b.w, c.x), mk3(c.y, c.z, c.w)};
+#pragma unroll
+            for (int t = 0; t < 4; t++) sum = (first_pass + 4 * g + t == 1) ? cs[t] : sum + cs[t];
+        }
+    } else {
+        for (int j = 0; j < batch; j++) {
+            const v3 c = mk3(pr[3 * j], pr[3 * j + 1], pr[3 * j + 2]);
+            sum = (first_pass + j == 1) ? c : sum + c;
+        }
     }
     img[0] = sum.x; img[1] = sum.y; img[2] = sum.z;
     if (write_u8 && P->out.image256)
