@@ -3,9 +3,10 @@
 Cornell + OBJ-mesh scene (BASELINE.json `metric`), on 1 GPU or tiled across N GPUs of one node.
 
 A step is one frame: 8 passes (batched into one persistent HIP launch plus an in-order accumulate)
-over the 1920x1080 frame and the 8-bit gamma output; with N > 1 each rank renders its interleaved 8-row bands and the float
-accumulation buffer is summed to rank 0 with one RCCL reduce (torch.distributed "nccl"), after
-which rank 0 writes the 8-bit image. Mrays/s = ray segments traced (the live-ray counts the
+over the 1920x1080 frame and the 8-bit gamma output; with N > 1 each rank renders its interleaved 8-row bands and
+rank 0 gathers the ranks' rows of the float accumulation buffer with one RCCL gather (torch.distributed
+"nccl"; PT_FRAME_COLLECTIVE=reduce: one reduce of the whole buffer instead), after which rank 0
+writes the 8-bit image. Mrays/s = ray segments traced (the live-ray counts the
 reference's thread_shrink returns, summed over passes and depths and over ranks) / wall time.
 
     python bench.py [--gpus N --steps K --warmup W]

@@ -3,16 +3,24 @@
 Every pixel's path depends only on (pass, global pixel index, depth) and the read-only scene
 (path_tracer_kernel.cu:324,415), so a frame shards with no exchange while rendering. Rank r of N
 owns the rows y with (y // band_rows) % N == r: interleaved bands balance sky against mesh. Each
-rank renders all passes of its rows into a full-size float accumulation buffer that is zero
-elsewhere, one reduce (RCCL over xGMI on the GPU box; any torch.distributed backend here) sums the
-buffers on rank 0, which then writes the 8-bit gamma image. Summing zeros is exact, so the result
-is bit-identical to one GPU.
+rank renders all passes of its rows into its full-size float accumulation buffer; then one
+collective brings the frame to rank 0, which writes the 8-bit gamma image:
+
+- "gather" (default): each rank packs its own rows (1/N of the frame) and rank 0 gathers them (RCCL
+  send/recv over xGMI on the GPU box: rank 0 receives N-1 pieces of 1/N of the frame, one per link)
+  and places them. Every pixel of rank 0's buffer is rewritten each frame.
+- "reduce" (PT_FRAME_COLLECTIVE=reduce): the buffers, zero outside each rank's rows, are summed on
+  rank 0 (a ring reduce moves about the whole buffer per rank); the buffer is cleared every frame.
+
+Either way the result is bit-identical to one GPU (disjoint pixels; summing zeros is exact).
 
 The renderer is anything with the pathtracerwithcuda_amd.Renderer frame interface (setup_frame,
 set_tiling, render, synchronize, finalize_u8); tests/test_multirank.py drives this same code
 with gloo on the CPU.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 
@@ -30,15 +38,19 @@ def owned_pixels(width: int, height: int, band_rows: int, band_count: int, band_
 
 
 class TiledFrame:
-    """One frame of `spp` passes on this rank's bands, reduced to rank 0 (world > 1)."""
+    """One frame of `spp` passes on this rank's bands, collected on rank 0 (world > 1)."""
 
-    def __init__(self, renderer, width: int, height: int, dist=None, band_rows: int = 8, device=None):
+    def __init__(self, renderer, width: int, height: int, dist=None, band_rows: int = 8, device=None,
+                 collective: str | None = None):
         self.r = renderer
         self.width, self.height = width, height
         self.dist = dist if (dist is not None and dist.is_available() and dist.is_initialized()) else None
         self.world = self.dist.get_world_size() if self.dist else 1
         self.rank = self.dist.get_rank() if self.dist else 0
         self.band_rows = band_rows
+        self.collective = collective or os.environ.get("PT_FRAME_COLLECTIVE", "gather")
+        if self.collective not in ("gather", "reduce"):
+            raise ValueError(f"unknown frame collective {self.collective!r}")
         self.image = None
         if self.world > 1:
             import torch
@@ -46,6 +58,13 @@ class TiledFrame:
             self.image = torch.zeros(width * height * 3, dtype=torch.float32, device=device)
             renderer.setup_frame(width, height, self.image.data_ptr())
             renderer.set_tiling(band_rows, self.world, self.rank)
+            # rows of every rank, and one equal-size (padded) packing buffer per rank for the gather
+            self.rows = [torch.as_tensor(owned_rows(height, band_rows, self.world, k), device=device)
+                         for k in range(self.world)]
+            most = max(len(rw) for rw in self.rows)
+            self.part = torch.zeros(most, width, 3, dtype=torch.float32, device=device)
+            self.parts = ([torch.zeros_like(self.part) for _ in range(self.world)]
+                          if self.rank == 0 else None)
         else:
             renderer.setup_frame(width, height)
 
@@ -57,7 +76,7 @@ class TiledFrame:
 
     def render(self, cam, cfg, spp: int) -> None:
         """Passes 1..spp; rank 0 ends with the full float image and its 8-bit output."""
-        if self.world > 1:
+        if self.world > 1 and self.collective == "reduce":
             # rows outside this rank's bands must be zero for the reduce, and rank 0's buffer still
             # holds the previous frame's sum: clear it (the renderer runs on its own stream: sync)
             self.image.zero_()
@@ -65,7 +84,17 @@ class TiledFrame:
         self.r.render(cam, cfg, 1, spp, write_u8=2 if self.world == 1 else 0)
         if self.world > 1:
             self.r.synchronize()
-            self.dist.reduce(self.image, dst=0)  # the one collective of the frame
+            if self.collective == "reduce":
+                self.dist.reduce(self.image, dst=0)  # the one collective of the frame
+            else:
+                img = self.image.view(self.height, self.width, 3)
+                mine = self.rows[self.rank]
+                self.part[:len(mine)] = img[mine]
+                self.dist.gather(self.part, gather_list=self.parts, dst=0)  # the one collective of the frame
+                if self.rank == 0:
+                    for k, rows in enumerate(self.rows):
+                        if k != 0:
+                            img[rows] = self.parts[k][:len(rows)]
             if self.rank == 0:
                 self._device_sync()
                 self.r.finalize_u8(cfg, spp)

@@ -65,14 +65,14 @@ def _setup():
     return cfg, cam
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, collective="gather"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         scene = _scene()
         cfg, cam = _setup()
         r = OracleFrameRenderer(scene)
-        frame = pt.TiledFrame(r, W, H, dist, BAND, device="cpu")
+        frame = pt.TiledFrame(r, W, H, dist, BAND, device="cpu", collective=collective)
         assert frame.world == world and frame.rank == rank
         for _ in range(2):  # a second frame must not see the first one's reduced sum (bench renders many)
             frame.render(cam, cfg, SPP)
@@ -100,18 +100,18 @@ def test_owned_pixels_partition_the_frame():
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_tiled_frame_equals_single_render(tmp_path):
-    world = 2
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+@pytest.mark.parametrize("world,collective", [(2, "gather"), (2, "reduce"), (3, "gather")])
+def test_two_rank_tiled_frame_equals_single_render(tmp_path, world, collective):
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), collective), nprocs=world, join=True,
                        start_method="spawn")
-    r0 = np.load(tmp_path / "rank0.npz")
-    r1 = np.load(tmp_path / "rank1.npz")
+    rs = [np.load(tmp_path / f"rank{k}.npz") for k in range(world)]
+    r0 = rs[0]
     cfg, cam = _setup()
     scene = _scene()  # keep alive: the view points into it
     ref, ref8, _ = oracle.render(scene.view, cam, cfg, 1, SPP)
     # rank 0 holds the reduced frame and its 8-bit image
     assert np.array_equal(r0["img"].view(np.uint32), ref.view(np.uint32))
     assert np.array_equal(r0["img8"], ref8)
-    # the two ranks' bands are disjoint and cover the frame (non-root buffers are scratch after a reduce)
-    assert not np.intersect1d(r0["owned"], r1["owned"]).size
-    assert len(r0["owned"]) + len(r1["owned"]) == W * H
+    # the ranks' bands are disjoint and cover the frame (non-root buffers are scratch after the collective)
+    owned = np.concatenate([r["owned"] for r in rs])
+    assert np.array_equal(np.sort(owned), np.arange(W * H))
