@@ -189,9 +189,17 @@ def main() -> int:
 
     import pathtracerwithcuda_amd as pt
 
+    # PT_BENCH_BACKEND / PT_BENCH_SHARE_GPU: rehearsal of the N > 1 path on a one-GPU box (gloo, every
+    # rank on device 0); the driver's multi-GPU runs use the defaults (RCCL, one GPU per rank)
+    backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
+    if os.environ.get("PT_BENCH_SHARE_GPU"):
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     r = pt.Renderer(local)
     r.set_schedule(args.schedule)
     schedule = r.schedule()
