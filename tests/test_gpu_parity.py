@@ -184,6 +184,46 @@ def test_material_and_config_variants(gpu, variant):
     assert_bitwise(img8, ref8, f"{variant} 8-bit")
 
 
+def _cube_at(x, y, z, s=0.18):
+    c = pt.cube_shape()
+    return pt.Shape((c.vertices * s + np.array([x, y, z], np.float32)).astype(np.float32), c.normals, c.uvs)
+
+
+@pytest.mark.parametrize("variant", ["many_meshes", "many_materials", "many_spheres"])
+def test_large_tables_and_many_meshes(gpu, variant):
+    """Scenes past the pass kernel's LDS tables: more than 64 meshes (ranges beyond the LDS copy come
+    from global memory), and more materials/spheres than the LDS tables hold (the launch falls back
+    to pass_kernel). Bit-exact like every other scene."""
+    rng = np.random.default_rng(11)
+    sc = pt.Scene()
+    walls = [sc.add_material(m) for m in ("wall_white", "wall_green", "wall_red", "wall_white", "wall_white")]
+    sc.add_mesh(pt.cornell_shapes(), walls, position=(0.0, -0.8, 1.0), scale=(0.1, 0.1, 0.3))
+    sc.add_mesh([pt.cube_shape()], [sc.add_material("light")], position=(0.0, 3.1, 0.0), scale=(0.85, 0.05, 0.85))
+    if variant == "many_meshes":  # 72 meshes of one cube each, in a grid, a few materials
+        mats = [sc.add_material(m) for m in ("red", "green", "gold", "diffuse_white")]
+        for k in range(70):
+            sc.add_mesh([_cube_at(-2.1 + 0.6 * (k % 10), -0.2 + 0.55 * (k // 10), -1.0)], [mats[k % 4]])
+    elif variant == "many_materials":  # one mesh of 360 cubes, each its own material
+        shapes, mats = [], []
+        for k in range(360):
+            shapes.append(_cube_at(-2.2 + 0.24 * (k % 20), -0.3 + 0.22 * (k // 20), -1.2, 0.08))
+            d = tuple(float(v) for v in rng.uniform(0.1, 0.9, 3))
+            mats.append(sc.add_material(pt.material((d, (0, 0, 0), (0.2, 0.2, 0.2), False, 0.3, 1.5, 0.0,
+                                                      (0, 0, 0), (0, 0, 0)))))
+        sc.add_mesh(shapes, mats)
+    else:  # 320 small spheres (each with its own material record)
+        for k in range(320):
+            sc.add_sphere((-2.2 + 0.28 * (k % 16), -0.3 + 0.2 * (k // 16), -1.0), 0.09,
+                          ("red", "gold", "glass", "iron")[k % 4])
+    sc.set_cube_map(pt.procedural_cube_map(16))
+    sc.build()
+    cfg = pt.configuration(max_tracer_depth=5)
+    cam = pt.camera(48, 32, **BENCH_CAM)
+    img, img8, ref, ref8, _ = render_both(gpu, sc, cam, cfg, passes=2)
+    assert_bitwise(img, ref, f"{variant} float")
+    assert_bitwise(img8, ref8, f"{variant} 8-bit")
+
+
 def test_full_size_pixel_subset(gpu):
     """At the benchmark size the oracle checks a random pixel subset (pixels are independent)."""
     sc = pt.cornell_scene(pt.torus_knot(), cube_length=512)
