@@ -18,9 +18,11 @@
  *
  * PINNING: the reference ships no tests, golden images or known-answer vectors, and its sources
  * cannot be compiled here without stand-in headers (CUDA runtime, FreeImage, backslash includes),
- * so oracle/_ref is not built. Pinned: the RNG streams and hash (rocThrust golden vectors,
- * tests/golden/rng_thrust.json). The full-path restatement is PARITY UNPINNED against reference
- * output; each function cites the reference file:line it follows.
+ * so oracle/_ref holds no build of the radiance loop. Pinned: the RNG streams and hash (rocThrust
+ * golden vectors, tests/golden/rng_thrust.json). The full-path restatement is PARITY UNPINNED
+ * against reference output; each function cites the reference file:line it follows.
+ * oracle/_ref/libptref.so (ref_harness.cpp) links the reference's vendored tinyobjloader, glm and
+ * lodepng to pin the host ingestion around the loop (tests/test_ref_pin.py).
  */
 #include <stdlib.h>
 #include <string.h>

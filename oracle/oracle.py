@@ -98,3 +98,75 @@ def math_eval(which: int, mode: str, x: np.ndarray):
     o1 = np.empty_like(x)
     lib().or_math_eval(which, MATH[mode], x.ctypes.data, len(x), o0.ctypes.data, o1.ctypes.data)
     return o0, o1
+
+
+# ---- oracle/_ref: the reference's vendored third-party libraries (tinyobjloader, glm, lodepng) ----
+REF_LIB = os.path.join(HERE, "_ref", "libptref.so")
+REF_SRC = "/root/reference/gpu_path_tracer"
+_ref = None
+
+
+def build_ref(force: bool = False) -> str | None:
+    """Builds oracle/_ref/libptref.so from the reference checkout's own vendored sources (Makefile
+    target `ref`). Returns None when neither the checkout nor a prebuilt library is present."""
+    if os.path.isdir(REF_SRC):
+        subprocess.run(["make", "-s", "-C", HERE] + (["-B"] if force else []) + ["ref"], check=True)
+    return REF_LIB if os.path.exists(REF_LIB) else None
+
+
+def ref_lib() -> C.CDLL | None:
+    global _ref
+    if _ref is None:
+        if build_ref() is None:
+            return None
+        h = C.CDLL(REF_LIB)
+        fp = C.POINTER(C.POINTER(C.c_float))
+        h.ptref_mesh_load.restype = C.c_int
+        h.ptref_mesh_load.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, fp, fp, fp,
+                                      C.POINTER(C.POINTER(C.c_int)), C.POINTER(C.c_int)]
+        h.ptref_png_decode.restype = C.c_int
+        h.ptref_png_decode.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                       C.POINTER(C.POINTER(C.c_ubyte))]
+        h.ptref_free.restype = None
+        h.ptref_free.argtypes = [C.c_void_p]
+        _ref = h
+    return _ref
+
+
+def ref_mesh_load(path: str, position=(0, 0, 0), scale=(1, 1, 1), rotate=(0, 0, 0)):
+    """Core/triangle_mesh.cpp:8-213 + :625-647 run on the real tinyobjloader and glm.
+    Returns (vertices (n,3,3), normals (n,3,3), uvs (n,3,2), shape_of_triangle (n,), has_uv)."""
+    h = ref_lib()
+    if h is None:
+        raise RuntimeError("oracle/_ref/libptref.so is not built (needs the reference checkout)")
+    arr = lambda t: (C.c_float * 3)(*t)
+    v, n, uv = C.POINTER(C.c_float)(), C.POINTER(C.c_float)(), C.POINTER(C.c_float)()
+    sh, has_uv = C.POINTER(C.c_int)(), C.c_int()
+    tri = h.ptref_mesh_load(path.encode(), arr(position), arr(scale), arr(rotate), C.byref(v), C.byref(n),
+                            C.byref(uv), C.byref(sh), C.byref(has_uv))
+    if tri < 0:
+        raise RuntimeError(f"reference load_obj({path!r}) fails")
+    try:
+        V = np.ctypeslib.as_array(v, (tri * 9,)).reshape(tri, 3, 3).copy() if tri else np.zeros((0, 3, 3), np.float32)
+        N = np.ctypeslib.as_array(n, (tri * 9,)).reshape(tri, 3, 3).copy() if tri else np.zeros((0, 3, 3), np.float32)
+        U = np.ctypeslib.as_array(uv, (tri * 6,)).reshape(tri, 3, 2).copy() if tri else np.zeros((0, 3, 2), np.float32)
+        S = np.ctypeslib.as_array(sh, (tri,)).copy() if tri else np.zeros(0, np.int32)
+    finally:
+        for p in (v, n, uv, sh):
+            h.ptref_free(p)
+    return V, N, U, S, bool(has_uv.value)
+
+
+def ref_png_decode(path: str) -> np.ndarray:
+    """lodepng::decode -> (H, W, 4) uint8 RGBA."""
+    h = ref_lib()
+    if h is None:
+        raise RuntimeError("oracle/_ref/libptref.so is not built (needs the reference checkout)")
+    w, hh, px = C.c_int(), C.c_int(), C.POINTER(C.c_ubyte)()
+    err = h.ptref_png_decode(path.encode(), C.byref(w), C.byref(hh), C.byref(px))
+    if err:
+        raise RuntimeError(f"lodepng error {err} on {path!r}")
+    try:
+        return np.ctypeslib.as_array(px, (hh.value, w.value, 4)).copy()
+    finally:
+        h.ptref_free(px)
