@@ -6,7 +6,9 @@ A step is one frame: 8 passes (batched into one persistent HIP launch plus an in
 over the 1920x1080 frame and the 8-bit gamma output; with N > 1 each rank renders its interleaved 8-row bands and
 rank 0 gathers the ranks' rows of the float accumulation buffer with one RCCL gather (torch.distributed
 "nccl"; PT_FRAME_COLLECTIVE=reduce: one reduce of the whole buffer instead), after which rank 0
-writes the 8-bit image. Mrays/s = ray segments traced (the live-ray counts the
+writes the 8-bit image. Frames are queued with no host synchronisation on two (three when N >= 4)
+renderer contexts, so one frame's tail overlaps the next frame's start (PT_BENCH_INFLIGHT=1: one at
+a time); the host-synchronised single-frame latency is reported beside it. Mrays/s = ray segments traced (the live-ray counts the
 reference's thread_shrink returns, summed over passes and depths and over ranks) / wall time.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -200,18 +202,22 @@ def main() -> int:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    r = pt.Renderer(local)
-    r.set_schedule(args.schedule)
-    schedule = r.schedule()
+    # frames in flight: one renderer context (own stream, image and pass buffers) per frame in flight,
+    # so the next frame's workgroups fill the previous frame's tail; 1 = one at a time
+    inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or (2 if world <= 2 else 3)
     wl = Workload(args.workload)
     scene, cfg, cam = wl.scene, wl.cfg, wl.cam
     width, height, spp = wl.width, wl.height, wl.spp
-    r.upload(scene, cfg)
-    tiled = pt.TiledFrame(r, width, height, dist if world > 1 else None, BAND_ROWS,
-                          device=f"cuda:{local}" if world > 1 else None)
-
-    def frame():
-        tiled.render(cam, cfg, spp)
+    rs, frames = [], []
+    for _ in range(inflight):
+        q = pt.Renderer(local)
+        q.set_schedule(args.schedule)
+        q.upload(scene, cfg)
+        rs.append(q)
+        frames.append(pt.TiledFrame(q, width, height, dist if world > 1 else None, BAND_ROWS,
+                                    device=f"cuda:{local}" if world > 1 else None))
+    r = rs[0]
+    schedule = r.schedule()
 
     # roofline inputs: one instrumented (untimed) frame for the visit counts
     r.set_instrumented(True)
@@ -221,22 +227,42 @@ def main() -> int:
     counts = r.stats_all()
     r.set_instrumented(False)
 
-    for _ in range(args.warmup):
-        frame()
-    r.stats_reset()
+    nframe = 0
+
+    def run(k: int) -> None:
+        nonlocal nframe
+        for _ in range(k):
+            frames[nframe % inflight].launch(cam, cfg, spp)
+            nframe += 1
+
+    run(args.warmup)
+    torch.cuda.synchronize()
+    for q in rs:
+        q.stats_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        frame()
+    run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    segments = r.stats()["segments"]
+    segments = sum(q.stats()["segments"] for q in rs)
     # dominant kernel: the pass kernel (persistent schedule) or the BVH-walk extend kernel (wavefront)
-    kernel_ms, launches = r.kernel_time_kind(0 if schedule == "persistent" else 1)
+    kind = 0 if schedule == "persistent" else 1
+    kernel_ms = sum(q.kernel_time_kind(kind)[0] for q in rs)
+    launches = sum(q.kernel_time_kind(kind)[1] for q in rs)
+    # single-frame latency (one frame at a time, host-synchronised), reported beside the throughput
+    lat_frames = min(3, args.steps)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    for _ in range(lat_frames):
+        frames[0].render(cam, cfg, spp)
+    if world > 1:
+        dist.barrier()
+    latency = (time.perf_counter() - t1) / max(lat_frames, 1)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
@@ -298,6 +324,8 @@ def main() -> int:
             "schedule": schedule,
             "band_rows": BAND_ROWS if world > 1 else None,
             "ms_per_frame": round(ms_per_step, 3),
+            "frames_in_flight": inflight,
+            "ms_per_frame_latency": round(latency * 1000.0, 3),
             "camera_samples_per_s_M": round(width * height * spp * args.steps / elapsed / 1e6, 3),
             "segments_per_frame": segments // max(args.steps, 1),
         },

@@ -54,6 +54,9 @@ int pt_render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_conf
 /* 8-bit gamma output of the current image for `pass` accumulated passes (after an external reduce). */
 int pt_finalize_u8(pt_context* ctx, const pt_configuration* config, int pass);
 int pt_synchronize(pt_context* ctx);
+/* The context's HIP stream (hipStream_t, non-blocking): callers order their own work on it (the
+ * multi-GPU frame packs, gathers and finalizes on it, so frames in flight need no host sync). */
+void* pt_stream_handle(pt_context* ctx);
 
 int pt_image_download(pt_context* ctx, pt_float3* image, pt_uchar3* image256);
 void* pt_image_device_ptr(pt_context* ctx);

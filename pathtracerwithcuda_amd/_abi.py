@@ -195,6 +195,7 @@ _PROTOS = {
                                    C.c_int]),
     "pt_finalize_u8": (C.c_int, [C.c_void_p, C.POINTER(Configuration), C.c_int]),
     "pt_synchronize": (C.c_int, [C.c_void_p]),
+    "pt_stream_handle": (C.c_void_p, [C.c_void_p]),
     "pt_image_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "pt_image_device_ptr": (C.c_void_p, [C.c_void_p]),
     "pt_image256_device_ptr": (C.c_void_p, [C.c_void_p]),

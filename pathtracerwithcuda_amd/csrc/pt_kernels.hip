@@ -246,7 +246,7 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
 template <int MINW, bool PROF, bool QN, int CHAIN, bool PF>
 __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
-                                                                int walk_steps, int tri_min, int walk_min) {
+                                                                int walk_steps, int tri_min, int walk_min, int tail) {
     const int lane = threadIdx.x & 63;
     const LaunchParams* P0 = params;
     const float clamp_hi = (float)P0->cfg.max_depth * 2.0f;
@@ -336,7 +336,11 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
 
         const unsigned long long ready = __ballot(mode == LANE_READY);
         const unsigned long long walking = __ballot(mode == LANE_WALK || mode == LANE_TRI);
-        if (ready && (__popcll(walking) <= (unsigned int)walk_min || __popcll(ready) >= (unsigned int)shade_min)) {
+        // once the launch's work is drained (wave-uniform) the wave only finishes its paths: its
+        // thresholds switch to the tail pair (tail = shade_min | walk_min << 8)
+        const unsigned int smin = drained ? (unsigned int)(tail & 0xff) : (unsigned int)shade_min;
+        const unsigned int wmin = drained ? (unsigned int)(tail >> 8) : (unsigned int)walk_min;
+        if (ready && (__popcll(walking) <= wmin || __popcll(ready) >= smin)) {
             if (PROF) { prof[3]++; prof[4] += (unsigned long long)__popcll(ready); }
             segments += (unsigned long long)__popcll(ready);
             bool alive = false;
@@ -632,7 +636,7 @@ bool unified_enabled() {
     return on != 0;
 }
 
-using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int, int);
+using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int, int, int);
 
 // PT_WALK_CHAIN: records per walk step (walk_box_chain); 1 = walk_box.
 static PassFnU pass_fn_u(int minw, bool qn) {
@@ -665,9 +669,12 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int 
         const LaunchParams* a0 = params_dev;
         static const int tri_min = env_int("PT_TRI_MIN", 4, 1, 64);
         static const int walk_min = env_int("PT_WALK_MIN", 8, 0, 64);
+        // PT_TAIL_SHADE_MIN / PT_TAIL_WALK_MIN: the shading thresholds of a wave once the work is drained
+        static const int tail_shade = env_int("PT_TAIL_SHADE_MIN", shade_min, 1, 64);
+        static const int tail_walk = env_int("PT_TAIL_WALK_MIN", walk_min, 0, 64);
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
-            a8 = walk_min;
-        void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8};
+            a8 = walk_min, a9 = tail_shade | (tail_walk << 8);
+        void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8, &a9};
         hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn), dim3(grid), dim3(PT_BLOCK), args,
                                        (size_t)lds_bytes, stream);
         if (e != hipSuccess) return e;

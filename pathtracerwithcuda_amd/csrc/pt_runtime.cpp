@@ -493,7 +493,13 @@ int pass_lds_bytes(const pt_context* ctx) {
 int pass_grid(pt_context* ctx) {
     const bool leaf1 = ctx->scene.leaf_size == 1, qn = use_qnodes(ctx);
     int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0][qn ? 1 : 0];
-    if (g == 0) g = pass_grid_size(leaf1, ctx->instrumented, qn, pass_lds_bytes(ctx));
+    if (g == 0) {
+        g = pass_grid_size(leaf1, ctx->instrumented, qn, pass_lds_bytes(ctx));
+        // PT_GRID_PCT: experiment knob, a percentage of the occupancy-sized grid
+        const char* e = getenv("PT_GRID_PCT");
+        const int pct = e ? atoi(e) : 100;
+        if (pct >= 5 && pct < 100) g = g * pct / 100 > 8 ? g * pct / 100 : 8;
+    }
     return g;
 }
 
@@ -811,6 +817,8 @@ extern "C" int pt_synchronize(pt_context* ctx) {
     PT_HIP(hipStreamSynchronize(ctx->stream));
     return PT_OK;
 }
+
+extern "C" void* pt_stream_handle(pt_context* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 extern "C" int pt_image_download(pt_context* ctx, pt_float3* image, pt_uchar3* image256) {
     if (!ctx || !ctx->image) return PT_E_STATE;

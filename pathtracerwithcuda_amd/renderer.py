@@ -98,6 +98,10 @@ class Renderer:
         check(self._lib.pt_image_download(self._ctx, img.ctypes.data, img8.ctypes.data), "pt_image_download")
         return img, img8
 
+    def stream_handle(self) -> int:
+        """The context's HIP stream (for torch.cuda.ExternalStream): work ordered on it follows the passes."""
+        return self._lib.pt_stream_handle(self._ctx) or 0
+
     def image_device_ptr(self) -> int:
         return self._lib.pt_image_device_ptr(self._ctx) or 0
 

@@ -263,6 +263,33 @@ def test_band_tiling_partitions_the_frame(gpu):
     assert np.array_equal(acc, full)
 
 
+@pytest.mark.parametrize("inflight", [2, 3])
+def test_frames_in_flight_equal_one_at_a_time(require_gpu, inflight):
+    """bench.py's frame pipeline: frames queued on several contexts with no host sync between them
+    (TiledFrame.launch) each end with the image of a frame rendered on its own, bit for bit."""
+    sc = pt.cornell_scene(pt.torus_knot(80, 24), cube_length=32)
+    cfg = pt.configuration(max_tracer_depth=8)
+    cam = pt.camera(96, 64, **BENCH_CAM)
+    ref, ref8, _ = oracle.render(sc.view, cam, cfg, 1, 4)
+    rs = [pt.Renderer(0) for _ in range(inflight)]
+    try:
+        frames = []
+        for q in rs:
+            q.upload(sc, cfg)
+            frames.append(pt.TiledFrame(q, 96, 64))
+        for i in range(2 * inflight + 1):
+            frames[i % inflight].launch(cam, cfg, 4)
+        for f in frames:
+            f.synchronize()
+        for q in rs:
+            img, img8 = q.download()
+            assert_bitwise(img.reshape(-1, 3), ref, "in-flight frame")
+            assert np.array_equal(img8.reshape(-1, 3), ref8)
+    finally:
+        for q in rs:
+            q.close()
+
+
 def test_reference_abi_path_tracer_kernel(gpu):
     """The drop-in entry point with host buffers, pass by pass, as Core/path_tracer.cpp:40-67 calls it."""
     sc = pt.cornell_scene(pt.torus_knot(50, 14), cube_length=32)

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Per-rank cost of the tiled frame, measured on ONE GPU: for N in 1, 2, 4, 8 the renderer is
+restricted to rank r's interleaved bands (pt_set_tiling) and one frame of the metric workload is
+timed for every r. The slowest rank's time against the 1-GPU frame / N is the strong-scaling
+ceiling of the tiled path before any collective (the driver measures the real N-GPU runs).
+
+    python tools/tile_scaling.py [--frames F]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import pathtracerwithcuda_amd as pt  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--counts", default="1,2,4,8")
+    ap.add_argument("--inflight", type=int, default=1, help="frames in flight (one renderer context each)")
+    ap.add_argument("--ranks-max", type=int, default=8, help="time at most this many ranks per N")
+    args = ap.parse_args()
+    wl = bench.Workload("metric")
+    rs = []
+    for _ in range(args.inflight):
+        r = pt.Renderer(0)
+        r.upload(wl.scene, wl.cfg)
+        r.setup_frame(wl.width, wl.height)
+        rs.append(r)
+    r = rs[0]
+    out = {}
+    base = None
+    for n in [int(x) for x in args.counts.split(",")]:
+        per_rank, kern = [], []
+        for k in range(min(n, args.ranks_max)):
+            for q in rs:
+                q.set_tiling(bench.BAND_ROWS, n, k)
+                q.render(wl.cam, wl.cfg, 1, wl.spp, write_u8=0)  # warm
+                q.synchronize()
+                q.stats_reset()
+            t0 = time.perf_counter()
+            for f in range(args.frames):
+                rs[f % len(rs)].render(wl.cam, wl.cfg, 1, wl.spp, write_u8=0)
+            for q in rs:
+                q.synchronize()
+            per_rank.append((time.perf_counter() - t0) / args.frames * 1e3)
+            kms, kn = r.kernel_time_kind(0)
+            kern.append(kms / max(kn, 1))
+        if base is None:
+            base = per_rank[0]
+        worst = max(per_rank)
+        out[n] = {"ms_per_rank": [round(x, 3) for x in per_rank], "worst_ms": round(worst, 3),
+                  "ideal_ms": round(base / n, 3),
+                  "kernel_ms_worst": round(max(kern), 3), "ceiling_efficiency": round(base / n / worst, 3)}
+        print(json.dumps({"n": n, **out[n]}), flush=True)
+    for q in rs:
+        q.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -16,6 +16,9 @@ cfg = pt.configuration(max_tracer_depth=bench.DEPTH)
 cam = pt.camera(bench.WIDTH, bench.HEIGHT, **bench.CAMERA)
 r.upload(scene, cfg)
 r.setup_frame(bench.WIDTH, bench.HEIGHT)
+TILE = int(os.environ.get("PT_UPROF_TILE", "1"))  # >1: rank 0's bands of an N-way tiled frame
+if TILE > 1:
+    r.set_tiling(bench.BAND_ROWS, TILE, 0)
 r.render(cam, cfg, 1, bench.SPP, write_u8=2)
 r.synchronize()
 r.stats_reset()
