@@ -33,6 +33,8 @@ KNOT = (350, 100)  # 70,000 triangles: the ~70k-triangle bunny stand-in (SURVEY.
 CAMERA = dict(pitch=0.08, radius=12.5, center=(0.0, 1.2, 0.0))
 BAND_ROWS = 8
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SIMDS = 256 * 4  # 256 CUs x 4 SIMDs
+CLOCK_HZ = 2.4e9  # MI355X_MICROARCH.md: max clock 2400 MHz
 
 
 def algorithmic_bytes(counts: dict, sphere_count: int, leaf_size: int, pixels: int, passes: int) -> float:
@@ -151,16 +153,16 @@ def cpu_baseline(scene, cam, cfg, threads: int) -> dict:
             "ms_per_frame": round(dt * 1000, 1)}
 
 
-def load_traffic(workload: str):
+def load_profile(workload: str) -> dict:
+    """The dominant kernel's PMC figures for this workload (profiles/traffic.json, written by
+    tools/traffic_summary.py from separate rocprofv3 --pmc passes): HBM bytes and VALU instructions."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
-        return None
+        return {}
     try:
-        d = json.load(open(path))
-        e = d.get(workload)
-        return float(e["hbm_bytes_per_launch"]) if e else None
+        return json.load(open(path)).get(workload) or {}
     except Exception:
-        return None
+        return {}
 
 
 def main() -> int:
@@ -302,7 +304,17 @@ def main() -> int:
         kernel_name = "extend_kernel<LEAF1=true,STATS=false>"
     achieved = bytes_per_launch / avg_launch_s / 1e9
     workload = wl.key
-    traffic = load_traffic(workload + ("" if schedule == "persistent" else "/wavefront"))
+    prof = load_profile(workload + ("" if schedule == "persistent" else "/wavefront"))
+    traffic = float(prof["hbm_bytes_per_launch"]) if prof.get("hbm_bytes_per_launch") else None
+    valu = None
+    if prof.get("valu_insts_per_launch"):
+        # VALU issue cycles (2 per wave64 instruction, MI355X_MICROARCH.md) over the SIMD cycles of one
+        # frame per rank at the 2.4 GHz clock: the share of the chip's VALU issue the path keeps busy
+        # (the profiled launch is the whole 1-GPU frame; a rank of N does 1/N of it)
+        insts = float(prof["valu_insts_per_launch"]) / world
+        busy = insts * 2.0 / (SIMDS * (elapsed / args.steps) * CLOCK_HZ)
+        valu = {"insts_per_frame_per_rank": round(insts), "busy_frac": round(busy, 4),
+                "source": "profiles/traffic.json (rocprofv3 --pmc SQ_INSTS_VALU)"}
     line = {
         "metric": "Mrays/sec + ms/frame @1920x1080, 8spp, 8-bounce; 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -336,6 +348,7 @@ def main() -> int:
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "valu": valu,
             "kernel": kernel_name,
             "avg_launch_ms": round(avg_launch_s * 1000, 4),
             "launches_per_frame": round(launches_per_frame, 3),

@@ -22,7 +22,7 @@ ap.add_argument("--round", default=None)
 args = ap.parse_args()
 
 agg = {}
-for sub, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+for sub, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE"), ("pmc_sq", "SQ_INSTS_VALU")):
     for f in glob.glob(os.path.join(args.src, sub, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
@@ -30,7 +30,8 @@ for sub, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
             k = r["Kernel_Name"].split("(")[0]
             agg.setdefault(k, {}).setdefault(counter, []).append(float(r["Counter_Value"]))
 
-summary = {k: {c: {"dispatches": len(v), "mean_kb": sum(v) / len(v)} for c, v in d.items()} for k, d in agg.items()}
+summary = {k: {c: {"dispatches": len(v), ("mean" if c.startswith("SQ_") else "mean_kb"): sum(v) / len(v)}
+                 for c, v in d.items()} for k, d in agg.items()}
 os.makedirs(args.out, exist_ok=True)
 json.dump(summary, open(os.path.join(args.out, "pmc_summary.json"), "w"), indent=1)
 
@@ -50,6 +51,9 @@ if args.workload:
         "source": f"{os.path.relpath(args.out)}/pmc_summary.json (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
                   "separate passes; FETCH_SIZE x2 gfx950 correction, KB x1024)",
         "kernel": k,
+        # wave-level VALU instructions per launch (pmc_sq pass), for bench.py's VALU-busy figure
+        "valu_insts_per_launch": (round(summary[k]["SQ_INSTS_VALU"]["mean"]) if "SQ_INSTS_VALU" in summary[k]
+                                  else None),
         "round": args.round or os.path.basename(os.path.normpath(args.out)),
     }
     json.dump(d, open(path, "w"), indent=1)
