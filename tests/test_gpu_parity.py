@@ -263,6 +263,42 @@ def test_band_tiling_partitions_the_frame(gpu):
     assert np.array_equal(acc, full)
 
 
+@pytest.mark.parametrize("case", ["sky_only", "spheres_only_sky_off", "depth0", "depth1", "tiny_2x2", "odd_pass_range"])
+def test_edge_cases(gpu, case):
+    """Degenerate inputs of the pass: a scene with nothing but the sky, no background at all, zero and
+    one bounce, a 2x2 frame, and a continuation range of passes that is not a power of two (3..9: the
+    launch splits it into batches of 4, 2 and 1 passes)."""
+    sc = pt.cornell_scene(pt.torus_knot(30, 10), cube_length=16)
+    cfg_kw = dict(max_tracer_depth=6)
+    W, H, first, passes = 24, 18, 1, 2
+    if case == "sky_only":
+        s0 = pt.Scene()
+        s0.set_cube_map(pt.procedural_cube_map(16))
+        sc = s0.build()
+    elif case == "spheres_only_sky_off":
+        sc = pt.cornell_spheres_scene(cube_length=0)
+        cfg_kw.update(use_sky_box=0, use_sky=0)
+    elif case == "depth0":
+        cfg_kw["max_tracer_depth"] = 0
+    elif case == "depth1":
+        cfg_kw["max_tracer_depth"] = 1
+    elif case == "tiny_2x2":
+        W, H = 2, 2
+    elif case == "odd_pass_range":
+        first, passes = 3, 7
+    cfg = pt.configuration(**cfg_kw)
+    cam = pt.camera(W, H, **BENCH_CAM)
+    gpu.upload(sc, cfg)
+    gpu.setup_frame(W, H)
+    if first > 1:
+        gpu.render(cam, cfg, 1, first - 1, write_u8=0)
+    gpu.render(cam, cfg, first, passes, write_u8=2)
+    img, img8 = gpu.download()
+    ref, ref8, _ = oracle.render(sc.view, cam, cfg, 1, first - 1 + passes)
+    assert_bitwise(img.reshape(-1, 3), ref, f"{case} float")
+    assert_bitwise(img8.reshape(-1, 3), ref8, f"{case} 8-bit")
+
+
 @pytest.mark.parametrize("inflight", [2, 3])
 def test_frames_in_flight_equal_one_at_a_time(require_gpu, inflight):
     """bench.py's frame pipeline: frames queued on several contexts with no host sync between them
