@@ -70,8 +70,15 @@ class TiledFrame:
                          for k in range(self.world)]
             most = max(len(rw) for rw in self.rows)
             self.part = torch.zeros(most, width, 3, dtype=torch.float32, device=device)
-            self.parts = ([torch.zeros_like(self.part) for _ in range(self.world)]
-                          if self.rank == 0 else None)
+            self.parts = None
+            if self.rank == 0:
+                # the gather lands in one [world, most, width, 3] buffer; one index map places every other
+                # rank's rows with a single gather + scatter (not one indexing pass per rank)
+                self.landing = torch.zeros(self.world, most, width, 3, dtype=torch.float32, device=device)
+                self.parts = list(self.landing.unbind(0))
+                src = [k * most + torch.arange(len(self.rows[k]), device=device) for k in range(1, self.world)]
+                self.src_rows = torch.cat(src)
+                self.dst_rows = torch.cat([self.rows[k] for k in range(1, self.world)])
             if self.image.is_cuda and hasattr(renderer, "stream_handle"):
                 self.stream = torch.cuda.ExternalStream(renderer.stream_handle(), device=self.image.device)
         else:
@@ -111,9 +118,7 @@ class TiledFrame:
                 self.part[:len(mine)] = img[mine]
                 self.dist.gather(self.part, gather_list=self.parts, dst=0)  # the one collective of the frame
                 if self.rank == 0:
-                    for k, rows in enumerate(self.rows):
-                        if k != 0:
-                            img[rows] = self.parts[k][:len(rows)]
+                    img[self.dst_rows] = self.landing.view(-1, self.width, 3)[self.src_rows]
             if self.rank == 0:
                 self.r.finalize_u8(cfg, spp)
 
