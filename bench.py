@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 WIDTH, HEIGHT, SPP, DEPTH = 1920, 1080, 8, 8
 KNOT = (350, 100)  # 70,000 triangles: the ~70k-triangle bunny stand-in
 CAMERA = dict(pitch=0.08, radius=12.5, center=(0.0, 1.2, 0.0))
-BAND_ROWS = 8
+BAND_ROWS = int(os.environ.get("PT_BAND_ROWS", "8"))  # rows per interleaved band of the tiled frame
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SIMDS = 256 * 4  # 256 CUs x 4 SIMDs
 CLOCK_HZ = 2.4e9  # MI355X_MICROARCH.md: max clock 2400 MHz

@@ -7,6 +7,10 @@
 #include "pt_work.h"
 
 #define PT_BLOCK 256
+// workgroup size of pass_kernel_u (the persistent unified pass kernel)
+#ifndef PT_UBLOCK
+#define PT_UBLOCK 256
+#endif
 
 namespace pt {
 

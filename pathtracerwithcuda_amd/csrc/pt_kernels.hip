@@ -244,7 +244,7 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
 // rounds, walk steps, walking lanes summed over steps, shading batches, lanes shaded, triangle
 // batches, lanes in triangle batches, lanes refilled.
 template <int MINW, bool PROF, bool QN, int CHAIN, bool PF>
-__global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
+__global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
                                                                 int walk_steps, int tri_min, int walk_min, int tail) {
     const int lane = threadIdx.x & 63;
@@ -258,13 +258,13 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel_u(const LaunchPara
     {
         const int2* mr = uniform_ptr(P0->sc.mesh_range);
         const int n = min(uniform_int(P0->sc.mesh_num), PT_LDS_MESHES);
-        for (int i = threadIdx.x; i < n; i += PT_BLOCK) lds_mesh[i] = mr[i];
+        for (int i = threadIdx.x; i < n; i += PT_UBLOCK) lds_mesh[i] = mr[i];
         const float4* ms = reinterpret_cast<const float4*>(uniform_ptr(P0->sc.materials));
         const int nm = uniform_int(P0->sc.material_num) * (int)(sizeof(DevMaterial) / 16);
-        for (int i = threadIdx.x; i < nm; i += PT_BLOCK) lds_dyn[i] = ms[i];
+        for (int i = threadIdx.x; i < nm; i += PT_UBLOCK) lds_dyn[i] = ms[i];
         const float4* sp = uniform_ptr(P0->sc.spheres);
         const int ns = uniform_int(P0->sc.sphere_num) * 2;
-        for (int i = threadIdx.x; i < ns; i += PT_BLOCK) lds_dyn[nm + i] = sp[i];
+        for (int i = threadIdx.x; i < ns; i += PT_UBLOCK) lds_dyn[nm + i] = sp[i];
         __syncthreads();
     }
     const float4* lds_spheres = lds_dyn + uniform_int(P0->sc.material_num) * (int)(sizeof(DevMaterial) / 16);
@@ -675,7 +675,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int 
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
             a8 = walk_min, a9 = tail_shade | (tail_walk << 8);
         void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8, &a9};
-        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn), dim3(grid), dim3(PT_BLOCK), args,
+        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn), dim3(grid), dim3(PT_UBLOCK), args,
                                        (size_t)lds_bytes, stream);
         if (e != hipSuccess) return e;
         return hipGetLastError();
@@ -714,7 +714,7 @@ int pass_grid_size(bool leaf1, bool stats, bool qn, int lds_bytes) {
     const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true), qn)
                        : (const void*)pass_fn(leaf1, stats, pass_min_waves(false), qn);
     const size_t lds = u ? (size_t)lds_bytes : 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, PT_BLOCK, lds) != hipSuccess || blocks <= 0) blocks = 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, u ? PT_UBLOCK : PT_BLOCK, lds) != hipSuccess || blocks <= 0) blocks = u ? 4 * PT_BLOCK / PT_UBLOCK : 4;
     if (cus <= 0) cus = 256;
     return cus * blocks;
 }
