@@ -65,17 +65,32 @@ def _setup():
     return cfg, cam
 
 
-def _worker(rank, world, port, out_dir, collective="gather"):
+def _worker(rank, world, port, out_dir, collective="gather", inflight=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         scene = _scene()
         cfg, cam = _setup()
-        r = OracleFrameRenderer(scene)
-        frame = pt.TiledFrame(r, W, H, dist, BAND, device="cpu", collective=collective)
-        assert frame.world == world and frame.rank == rank
-        for _ in range(2):  # a second frame must not see the first one's reduced sum (bench renders many)
-            frame.render(cam, cfg, SPP)
+        if inflight == 1:
+            r = OracleFrameRenderer(scene)
+            frame = pt.TiledFrame(r, W, H, dist, BAND, device="cpu", collective=collective)
+            assert frame.world == world and frame.rank == rank
+            for _ in range(2):  # a second frame must not see the first one's reduced sum (bench renders many)
+                frame.render(cam, cfg, SPP)
+        else:
+            # bench.py's frames in flight: one renderer + TiledFrame per frame in flight, frames queued with
+            # launch() round-robin and synchronised at the end; every context must hold a whole frame
+            rs = [OracleFrameRenderer(scene) for _ in range(inflight)]
+            frames = [pt.TiledFrame(q, W, H, dist, BAND, device="cpu", collective=collective) for q in rs]
+            for i in range(2 * inflight + 1):
+                frames[i % inflight].launch(cam, cfg, SPP)
+            for f in frames:
+                f.synchronize()
+            if rank == 0:
+                for q in rs[1:]:
+                    assert np.array_equal(q.img.view(np.uint32), rs[0].img.view(np.uint32))
+                    assert np.array_equal(q.img8, rs[0].img8)
+            r = rs[0]
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), img=r.img.copy(), img8=r.img8.copy(),
                  owned=pt.owned_pixels(W, H, BAND, world, rank))
     finally:
@@ -100,9 +115,10 @@ def test_owned_pixels_partition_the_frame():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,collective", [(2, "gather"), (2, "reduce"), (3, "gather")])
-def test_two_rank_tiled_frame_equals_single_render(tmp_path, world, collective):
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), collective), nprocs=world, join=True,
+@pytest.mark.parametrize("world,collective,inflight", [(2, "gather", 1), (2, "reduce", 1), (3, "gather", 1),
+                                                       (2, "gather", 2), (2, "reduce", 3)])
+def test_two_rank_tiled_frame_equals_single_render(tmp_path, world, collective, inflight):
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), collective, inflight), nprocs=world, join=True,
                        start_method="spawn")
     rs = [np.load(tmp_path / f"rank{k}.npz") for k in range(world)]
     r0 = rs[0]
