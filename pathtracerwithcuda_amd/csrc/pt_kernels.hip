@@ -663,8 +663,9 @@ static bool use_unified(bool leaf1, bool stats, bool qn, int lds_bytes) {
 hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int first_pass, int batch_log2,
                        int write_u8, int grid, bool stats, int lds_bytes, hipStream_t stream) {
     if (use_unified(leaf1, stats, qn, lds_bytes)) {
-        static const int chunk = env_int("PT_CHUNK_MEGA", 32, 0, 4096);
-        static const int shade_min = env_int("PT_SHADE_MIN", 32, 1, 64);
+        // 64-unit chunks and a 28-lane shading batch: measured best with frames in flight
+        static const int chunk = env_int("PT_CHUNK_MEGA", 64, 0, 4096);
+        static const int shade_min = env_int("PT_SHADE_MIN", 28, 1, 64);
         static const int walk_steps = env_int("PT_WALK_STEPS", 10, 1, 64);
         const LaunchParams* a0 = params_dev;
         static const int tri_min = env_int("PT_TRI_MIN", 4, 1, 64);
