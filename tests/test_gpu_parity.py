@@ -349,6 +349,44 @@ def test_reference_abi_path_tracer_kernel(gpu):
     assert_bitwise(got8, ref8, "ABI 8-bit")
 
 
+def test_reference_abi_sees_in_place_edits(require_gpu):
+    """The reference ABI keeps the resident scene when a pass-1 call re-sends identical content, and must
+    re-read it after an in-place edit (the reference's editor writes materials and spheres into the same
+    managed buffers, then resets pass_counter): the edited frame equals the oracle's, and so does the
+    unedited one rendered again after it."""
+    sc = pt.cornell_scene(pt.torus_knot(40, 12), cube_length=16)
+    cfg = pt.configuration(max_tracer_depth=5)
+    cam = pt.camera(32, 24, **BENCH_CAM)
+    n = 32 * 24
+    img = (pt._abi.Float3 * n)()
+    img8 = (pt._abi.UChar3 * n)()
+    scratch = [C.c_void_p() for _ in range(5)]
+    lib = pt.lib()
+    lib.path_tracer_kernel_memory_allocate(*[C.byref(s) for s in scratch], n)
+    v = sc.view
+
+    def frame(passes=2):
+        for p in range(1, passes + 1):
+            lib.path_tracer_kernel(v.mesh_num, v.bvh_nodes, v.triangles, v.sphere_num, v.spheres, n, img, img8, p,
+                                   C.byref(cam), v.sky_cube_map, *scratch, v.mesh_textures, C.byref(cfg))
+        return np.frombuffer(img, np.float32).reshape(-1, 3).copy()
+
+    try:
+        base = frame()
+        assert_bitwise(frame(), base, "unchanged scene, second frame")
+        old = v.spheres[0].mat.diffuse_color.x, v.spheres[0].radius
+        v.spheres[0].mat.diffuse_color.x = 0.123
+        v.spheres[0].radius = old[1] * 1.3
+        edited = frame()
+        ref, _, _ = oracle.render(v, cam, cfg, 1, 2)
+        assert_bitwise(edited, ref, "after in-place edit")
+        assert not np.array_equal(edited, base)
+        v.spheres[0].mat.diffuse_color.x, v.spheres[0].radius = old
+        assert_bitwise(frame(), base, "edit undone")
+    finally:
+        lib.path_tracer_kernel_memory_free(*scratch)
+
+
 def test_thread_shrink_matches_stable_remove_if(gpu):
     import torch
     rng = np.random.default_rng(5)
