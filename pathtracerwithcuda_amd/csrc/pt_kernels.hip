@@ -668,7 +668,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int 
         static const int shade_min = env_int("PT_SHADE_MIN", 28, 1, 64);
         static const int walk_steps = env_int("PT_WALK_STEPS", 10, 1, 64);
         const LaunchParams* a0 = params_dev;
-        static const int tri_min = env_int("PT_TRI_MIN", 4, 1, 64);
+        static const int tri_min = env_int("PT_TRI_MIN", 6, 1, 64);  // measured best with frames in flight
         static const int walk_min = env_int("PT_WALK_MIN", 8, 0, 64);
         // PT_TAIL_SHADE_MIN / PT_TAIL_WALK_MIN: the shading thresholds of a wave once the work is drained
         static const int tail_shade = env_int("PT_TAIL_SHADE_MIN", shade_min, 1, 64);
