@@ -153,6 +153,21 @@ def cpu_baseline(scene, cam, cfg, threads: int) -> dict:
             "ms_per_frame": round(dt * 1000, 1)}
 
 
+def host_threads(requested: int = 0) -> tuple[int, str]:
+    """The host cores this job may use: every CPU of its affinity mask, unless the environment limits
+    OpenMP (the GPU boxes export OMP_NUM_THREADS = their CPU share for one GPU)."""
+    if requested:
+        return requested, "--cpu-threads"
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < aff:
+        return int(omp), f"OMP_NUM_THREADS={omp} (this job's CPU share; {aff} CPUs in the affinity mask)"
+    return aff, f"all {aff} CPUs of the affinity mask"
+
+
 def load_profile(workload: str) -> dict:
     """The dominant kernel's PMC figures for this workload (profiles/traffic.json, written by
     tools/traffic_summary.py from separate rocprofv3 --pmc passes): HBM bytes and VALU instructions."""
@@ -255,8 +270,11 @@ def main() -> int:
     kind = 0 if schedule == "persistent" else 1
     kernel_ms = sum(q.kernel_time_kind(kind)[0] for q in rs)
     launches = sum(q.kernel_time_kind(kind)[1] for q in rs)
-    # single-frame latency (one frame at a time, host-synchronised), reported beside the throughput
-    lat_frames = min(3, args.steps)
+    # single-frame latency (one frame at a time, host-synchronised), reported beside the throughput; the
+    # dominant kernel's launch duration for the roofline is taken here too, with no other frame in flight
+    # (with frames in flight the HIP events of one launch also span the overlapping launch's work)
+    lat_frames = max(3, min(5, args.steps))
+    r.stats_reset()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
@@ -265,6 +283,7 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     latency = (time.perf_counter() - t1) / max(lat_frames, 1)
+    solo_ms, solo_launches = r.kernel_time_kind(kind)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
@@ -289,7 +308,7 @@ def main() -> int:
 
     value = segments / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1000.0
-    avg_launch_s = kernel_ms / max(launches, 1) / 1000.0
+    avg_launch_s = solo_ms / max(solo_launches, 1) / 1000.0  # one frame at a time (see above)
     launches_per_frame = launches / max(args.steps, 1)
     if schedule == "persistent":
         # one launch = a batch of passes over the frame (this rank's bands when tiled)
@@ -302,19 +321,24 @@ def main() -> int:
         # one launch = one depth of one pass
         bytes_per_launch = extend_bytes(counts, scene.view.sphere_num) / world / launches_per_frame
         kernel_name = "extend_kernel<LEAF1=true,STATS=false>"
-    achieved = bytes_per_launch / avg_launch_s / 1e9
     workload = wl.key
     prof = load_profile(workload + ("" if schedule == "persistent" else "/wavefront"))
-    traffic = float(prof["hbm_bytes_per_launch"]) if prof.get("hbm_bytes_per_launch") else None
-    valu = None
-    if prof.get("valu_insts_per_launch"):
-        # VALU issue cycles (2 per wave64 instruction, MI355X_MICROARCH.md) over the SIMD cycles of one
-        # frame per rank at the 2.4 GHz clock: the share of the chip's VALU issue the path keeps busy
-        # (the profiled launch is the whole 1-GPU frame; a rank of N does 1/N of it)
-        insts = float(prof["valu_insts_per_launch"]) / world
-        busy = insts * 2.0 / (SIMDS * (elapsed / args.steps) * CLOCK_HZ)
-        valu = {"insts_per_frame_per_rank": round(insts), "busy_frac": round(busy, 4),
-                "source": "profiles/traffic.json (rocprofv3 --pmc SQ_INSTS_VALU)"}
+    # the profiled launch is the whole 1-GPU frame; a rank of N runs 1/N of it
+    traffic = float(prof["hbm_bytes_per_launch"]) / world if prof.get("hbm_bytes_per_launch") else None
+    valu_insts = float(prof["valu_insts_per_launch"]) / world if prof.get("valu_insts_per_launch") else None
+    # The resource that binds this kernel is VALU issue behind a dependent-load chain, not HBM
+    # (DESIGN.md §4): a wave64 VALU instruction issues over 2 cycles of its SIMD-32
+    # (MI355X_MICROARCH.md, Wave scheduling), so the chip issues at most SIMDS x clock / 2 wave-level
+    # VALU instructions per second. achieved = SQ_INSTS_VALU per launch (rocprofv3 --pmc, profiles/)
+    # / the launch's duration measured here with HIP events on the renderer's stream, one frame in flight.
+    valu_peak = SIMDS * CLOCK_HZ / 2.0 / 1e9  # G wave-instructions / s
+    valu_achieved = valu_insts / avg_launch_s / 1e9 if valu_insts else None
+    hbm = None
+    if traffic is not None:
+        hbm_gbs = traffic / avg_launch_s / 1e9
+        hbm = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": round(traffic),
+               "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (gfx950 FETCH x2), profiles/traffic.json"}
     line = {
         "metric": "Mrays/sec + ms/frame @1920x1080, 8spp, 8-bounce; 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -342,25 +366,31 @@ def main() -> int:
             "segments_per_frame": segments // max(args.steps, 1),
         },
         "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "valu": valu,
+            "bound": "valu",
+            "achieved": round(valu_achieved, 1) if valu_achieved else None,
+            "peak": valu_peak,
+            "unit": "G VALU wave-instructions/s",
+            "frac": round(valu_achieved / valu_peak, 4) if valu_achieved else None,
+            "traffic": round(traffic) if traffic is not None else None,
+            "hbm": hbm,
+            "valu_insts_per_launch": round(valu_insts) if valu_insts else None,
             "kernel": kernel_name,
             "avg_launch_ms": round(avg_launch_s * 1000, 4),
+            "avg_launch_source": "HIP events on the renderer stream, one frame in flight",
+            "avg_launch_ms_frames_in_flight": round(kernel_ms / max(launches, 1), 4),
             "launches_per_frame": round(launches_per_frame, 3),
+            # SURVEY.md §8(d)'s reference-layout bytes: what the reference's AoS walk would load per launch,
+            # mostly served by L1/L2/MALL here; a cache-level figure, not an HBM fraction
             "algorithmic_bytes_per_launch": round(bytes_per_launch),
             "counts_per_frame": counts,
         },
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline and args.workload == "metric":
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        threads, why = host_threads(args.cpu_threads)
         line["cpu_baseline"] = cpu_baseline(scene, cam, cfg, threads)
         line["cpu_baseline"]["cpu"] = platform.processor() or platform.machine()
+        line["cpu_baseline"]["threads_from"] = why
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -50,9 +50,13 @@ def lib() -> C.CDLL:
 
 
 def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.ndarray | None = None,
-           rng: str = "thrust", math: str = "cephes", threads: int = 0, with_u8: bool = True):
+           rng: str = "thrust", math: str = "cephes", threads: int = 0, with_u8: bool = True,
+           image: np.ndarray | None = None, image256: np.ndarray | None = None):
     """Run passes first_pass..first_pass+pass_count-1 over all pixels (or the given pixel indices).
 
+    `image` / `image256` (optional, float32 / uint8, n*3 contiguous) are the caller's running sum and
+    8-bit buffers, updated in place with the reference's pass_counter semantics (a pass > 1 adds
+    into the running sum): the CPU twin's view of Core/path_tracer.cpp:71-91.
     Returns (image float32 [n,3], image256 uint8 [n,3] or None, stats dict)."""
     L = lib()
     if pixels is None:
@@ -61,8 +65,16 @@ def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.
     else:
         plist = np.ascontiguousarray(pixels, np.int32)
         n = len(plist)
-    img = np.zeros((n, 3), np.float32)
-    img8 = np.zeros((n, 3), np.uint8) if with_u8 else None
+    if image is not None:
+        assert image.dtype == np.float32 and image.flags.c_contiguous and image.size == n * 3
+        img = image.reshape(n, 3)
+    else:
+        img = np.zeros((n, 3), np.float32)
+    if image256 is not None:
+        assert image256.dtype == np.uint8 and image256.flags.c_contiguous and image256.size == n * 3
+        img8 = image256.reshape(n, 3)
+    else:
+        img8 = np.zeros((n, 3), np.uint8) if with_u8 else None
     stats = (C.c_ulonglong * 3)()
     rc = L.or_render(view.mesh_num, C.cast(view.bvh_nodes, C.c_void_p), C.cast(view.triangles, C.c_void_p),
                      view.sphere_num, C.cast(view.spheres, C.c_void_p), C.cast(view.sky_cube_map, C.c_void_p),

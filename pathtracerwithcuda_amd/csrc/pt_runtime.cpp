@@ -562,7 +562,6 @@ int ensure_wave(pt_context* ctx, int units, int depth) {
     for (int i = 0; i < 8; i++) { off[i] = total; total = (total + sizes[i] + 255) & ~(size_t)255; }
     if (total > ctx->wave_bytes) {
         if (ctx->wave_mem) (void)hipFree(ctx->wave_mem);
-    if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
         ctx->wave_mem = nullptr;
         ctx->wave_bytes = 0;
         PT_HIP(hipMalloc(&ctx->wave_mem, total));
@@ -766,6 +765,7 @@ extern "C" void pt_context_destroy(pt_context* ctx) {
     if (ctx->stats) (void)hipFree(ctx->stats);
     if (ctx->params) (void)hipFree(ctx->params);
     if (ctx->wave_mem) (void)hipFree(ctx->wave_mem);
+    if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
     if (ctx->shrink_buf) (void)hipFree(ctx->shrink_buf);
     if (ctx->shrink_tiles) (void)hipFree(ctx->shrink_tiles);
     if (ctx->shrink_total) (void)hipFree(ctx->shrink_total);
@@ -1008,15 +1008,36 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
     uint8_t* own256 = ctx->image256;
     if (direct) ctx->image256 = (uint8_t*)image_pixels_256;
     ctx->tiling.band_count = 1;
-    rc = render_passes(ctx, &cam, &config, pass_counter, 1, 1);
+    const size_t px = (size_t)pixel_count;
+    if (!direct && pass_counter != 1) {
+        // A pass after the first adds into the CALLER's running sum (path_tracer_kernel.cu:644-651), and
+        // the caller may have advanced it on the host in between: Core/path_tracer.cpp:46-91 switches
+        // between this entry and the CPU twin path_tracer_cpu per pass on the same (managed) buffers.
+        // So the mirror is refreshed from the caller's buffer before every continuation pass.
+        if (hipMemcpyAsync(ctx->image, image_pixels, px * 12, hipMemcpyDefault, ctx->stream) != hipSuccess) {
+            set_error("[Hip]Error uploading the caller's running sum");
+            rc = PT_E_HIP;
+        }
+    }
+    if (rc == PT_OK) rc = render_passes(ctx, &cam, &config, pass_counter, 1, 1);
     if (rc == PT_OK) {
-        if (!direct) rc = pt_image_download(ctx, image_pixels, image_pixels_256);
-        else if (hipStreamSynchronize(ctx->stream) != hipSuccess) { set_error("[Hip]Error synchronize"); rc = PT_E_HIP; }
+        if (!direct) {
+            hipError_t e = hipMemcpyAsync(image_pixels, ctx->image, px * 12, hipMemcpyDefault, ctx->stream);
+            if (e == hipSuccess) e = hipMemcpyAsync(image_pixels_256, ctx->image256, px * 3, hipMemcpyDefault, ctx->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+            if (e != hipSuccess) { set_error("[Hip]Error %s downloading the image", hipGetErrorString(e)); rc = PT_E_HIP; }
+        } else if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
+            set_error("[Hip]Error synchronize");
+            rc = PT_E_HIP;
+        }
     }
     if (direct) { ctx->image256 = own256; ctx->image = nullptr; ctx->image_cap = 0; ctx->own_image = false; }
     if (rc != PT_OK) report("path_tracer_kernel");
 }
 
+// Kernel/path_tracer_kernel.cu:782-796: cudaMallocManaged. The caller hands the same scratch to the CPU
+// twin (Core/path_tracer.cpp:71-91), which reads and writes it on the host, so it is managed here too;
+// the HIP kernels keep path state in registers and never touch it.
 extern "C" void path_tracer_kernel_memory_allocate(pt_float3** not_absorbed, pt_float3** accumulated, pt_ray** rays,
                                                    int** energy, pt_scattering** scatterings, int pixel_count) {
     size_t n = pixel_count > 0 ? (size_t)pixel_count : 1;
@@ -1028,7 +1049,7 @@ extern "C" void path_tracer_kernel_memory_allocate(pt_float3** not_absorbed, pt_
     for (auto& x : a) {
         if (!x.p) continue;
         *x.p = nullptr;
-        hipError_t e = hipMalloc(x.p, x.b);
+        hipError_t e = hipMallocManaged(x.p, x.b, hipMemAttachGlobal);
         if (e != hipSuccess) std::fprintf(stderr, "[Hip]Error %s in path_tracer_kernel_memory_allocate\n", hipGetErrorString(e));
     }
 }

@@ -1,0 +1,59 @@
+"""Worker of tests/test_gpu_multirank.py, launched N times by torch.distributed.run on ONE GPU (every
+rank on cuda:0, gloo between them): the bench.py frame pipeline (TiledFrame over renderer contexts,
+two frames in flight, rank 0 collecting the frame) on the HIP renderer. Rank 0 saves each context's
+float image and 8-bit image for the test to compare with the oracle.
+
+    worker.py OUT_PREFIX COLLECTIVE FRAMES
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+W, H, SPP = 96, 64, 4
+CAM = dict(pitch=0.08, radius=12.5, center=(0.0, 1.2, 0.0))
+
+
+def scene():
+    import pathtracerwithcuda_amd as pt
+    return pt.cornell_scene(pt.torus_knot(80, 24), cube_length=32)
+
+
+def main() -> int:
+    out, collective, frames = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    import torch.distributed as dist
+
+    import pathtracerwithcuda_amd as pt
+
+    dist.init_process_group("gloo")
+    rank = dist.get_rank()
+    sc = scene()
+    cfg = pt.configuration(max_tracer_depth=8)
+    cam = pt.camera(W, H, **CAM)
+    rs, fr = [], []
+    for _ in range(2):  # two frames in flight, one renderer context each (bench.py)
+        r = pt.Renderer(0)
+        r.upload(sc, cfg)
+        rs.append(r)
+        fr.append(pt.TiledFrame(r, W, H, dist, 8, device="cuda:0", collective=collective))
+    for i in range(frames):
+        fr[i % 2].launch(cam, cfg, SPP)
+    for f in fr:
+        f.synchronize()
+    if rank == 0:
+        for k, (r, f) in enumerate(zip(rs, fr)):
+            _, img8 = r.download()
+            np.save(f"{out}_{k}_f.npy", f.image.cpu().numpy().reshape(-1, 3))
+            np.save(f"{out}_{k}_u8.npy", img8.reshape(-1, 3))
+    dist.barrier()
+    for r in rs:
+        r.close()
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,46 @@
+"""The N > 1 frame pipeline on the HIP renderer: 2 and 3 ranks, every rank on cuda:0 (this pool's boxes
+have one GPU), gloo between the ranks, through the same TiledFrame/renderer code bench.py runs with
+RCCL on an 8-GPU node (band tiling, two frames in flight on their own HIP streams, the frame's one
+collective — a gather of the ranks' rows or a reduce of the float buffer — and rank 0's 8-bit
+output). Rank 0's images must equal the oracle's single-frame render bit for bit."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+import pathtracerwithcuda_amd as pt
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import gpu_multirank_worker as worker  # noqa: E402
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("ranks,collective", [(2, "gather"), (3, "reduce")])
+def test_tiled_frames_on_hip_equal_the_oracle(require_gpu, tmp_path, ranks, collective):
+    out = str(tmp_path / "mr")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(HERE, "gpu_multirank_worker.py"), out, collective, "5"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert res.returncode == 0, res.stderr[-4000:]
+    sc = worker.scene()
+    cfg = pt.configuration(max_tracer_depth=8)
+    cam = pt.camera(worker.W, worker.H, **worker.CAM)
+    ref, ref8, _ = oracle.render(sc.view, cam, cfg, 1, worker.SPP)
+    for k in range(2):
+        img = np.load(f"{out}_{k}_f.npy")
+        img8 = np.load(f"{out}_{k}_u8.npy")
+        assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), f"context {k}: float image"
+        assert np.array_equal(img8, ref8), f"context {k}: 8-bit image"

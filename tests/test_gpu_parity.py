@@ -239,6 +239,116 @@ def test_full_size_pixel_subset(gpu):
     assert_bitwise(img8.reshape(-1, 3)[sel], ref8, "subset 8-bit")
 
 
+@pytest.fixture(scope="module")
+def bench_gpu(require_gpu):
+    """The schedule bench.py times (the library default: persistent pass_kernel_u, 8 passes batched)."""
+    r = pt.Renderer(0)
+    assert r.schedule() == "persistent"
+    yield r
+    r.close()
+
+
+@pytest.fixture(scope="module")
+def c4_workload():
+    import bench
+    return bench.Workload("c4")
+
+
+def _subset(w, h, n=3000, seed=0):
+    return np.sort(np.random.default_rng(seed).choice(w * h, n, replace=False)).astype(np.int32)
+
+
+def _render_workload_subset(r, wl, passes=8, npx=20000, seed=0):
+    """One frame of `passes` passes through the batched launch bench.py times, checked on a pixel
+    subset against the oracle (float running sum and the 8-bit output of the last pass). Returns the
+    launch counts by kind so the caller can pin the launch shape."""
+    r.upload(wl.scene, wl.cfg)
+    r.setup_frame(wl.width, wl.height)
+    r.stats_reset()
+    r.render(wl.cam, wl.cfg, 1, passes, write_u8=2)
+    r.synchronize()
+    launches = {k: r.kernel_time_kind(k)[1] for k in (0, 3)}
+    img, img8 = r.download()
+    sel = _subset(wl.width, wl.height, npx, seed)
+    ref, ref8, st = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, passes, pixels=sel)
+    assert_bitwise(img.reshape(-1, 3)[sel], ref, f"{wl.name} subset float")
+    assert_bitwise(img8.reshape(-1, 3)[sel], ref8, f"{wl.name} subset 8-bit")
+    assert st["segments"] > npx * passes
+    return launches, img
+
+
+def test_metric_frame_at_the_bench_launch_shape(bench_gpu):
+    """bench.py's exact step: the metric workload (1920x1080, Cornell + 70k-triangle knot, depth 8), all
+    8 passes in ONE persistent launch (batch_log2 = 3) plus one accumulate_kernel launch (its four-pass
+    float4 groups, path_tracer_kernel.cu:644-651 applied pass after pass), then the 8-bit output."""
+    import bench
+    wl = bench.Workload("metric")
+    launches, _ = _render_workload_subset(bench_gpu, wl, passes=8, npx=30000)
+    assert launches == {0: 1, 3: 1}, launches
+
+
+def test_c4_800k_sss_frame(bench_gpu, c4_workload):
+    """BASELINE config C4: the 800k-triangle knot with the DragonGreen subsurface medium at 1920x1080,
+    depth 8, 8 passes in one launch, pixel subset against the oracle."""
+    assert c4_workload.scene.triangle_count >= 800000
+    launches, _ = _render_workload_subset(bench_gpu, c4_workload, passes=8)
+    assert launches == {0: 1, 3: 1}, launches
+
+
+def test_c5_4k_textured_depth12_frame(bench_gpu):
+    """BASELINE config C5: three textured knots + a textured cube (diffuse and specular maps) at 3840x2160,
+    depth 12, 8 passes in one launch, pixel subset against the oracle."""
+    import bench
+    wl = bench.Workload("c5")
+    assert wl.depth == 12 and (wl.width, wl.height) == (3840, 2160)
+    launches, _ = _render_workload_subset(bench_gpu, wl, passes=8)
+    assert launches == {0: 1, 3: 1}, launches
+
+
+@pytest.mark.parametrize("bands", [4, 8])
+def test_c4_band_tiling_partitions_the_frame(bench_gpu, c4_workload, bands):
+    """The multi-GPU partition on the C4 scene at the bench's 8-row bands: every rank's share rendered
+    with pt_set_tiling equals the single-context frame on its rows, bit for bit, and the shares cover
+    the frame."""
+    wl = c4_workload
+    r = bench_gpu
+    r.upload(wl.scene, wl.cfg)
+    r.setup_frame(wl.width, wl.height)
+    r.render(wl.cam, wl.cfg, 1, 8, write_u8=0)
+    full, _ = r.download()
+    owned = np.zeros(wl.height, bool)
+    try:
+        for k in range(bands):
+            r.set_tiling(8, bands, k)
+            r.render(wl.cam, wl.cfg, 1, 8, write_u8=0)
+            part, _ = r.download()
+            rows = pt.owned_rows(wl.height, 8, bands, k)
+            assert not owned[rows].any()
+            owned[rows] = True
+            assert np.array_equal(part[rows], full[rows]), f"band owner {k} of {bands}"
+    finally:
+        r.set_tiling(1, 1, 0)
+    assert owned.all()
+
+
+def test_schedule_switch_on_one_context(require_gpu):
+    """persistent -> wavefront (a larger frame grows the wavefront buffers) -> persistent on ONE context:
+    each render equals the oracle (the batched pass buffer must survive the wavefront schedule's growth)."""
+    sc = pt.cornell_scene(pt.torus_knot(40, 12), cube_length=16)
+    cfg = pt.configuration(max_tracer_depth=5)
+    r = pt.Renderer(0)
+    try:
+        for sched, (w, h) in (("persistent", (48, 32)), ("wavefront", (96, 64)), ("persistent", (48, 32)),
+                              ("persistent", (96, 64))):
+            r.set_schedule(sched)
+            cam = pt.camera(w, h, **BENCH_CAM)
+            img, img8, ref, ref8, _ = render_both(r, sc, cam, cfg, passes=4)
+            assert_bitwise(img, ref, f"{sched} {w}x{h} float")
+            assert_bitwise(img8, ref8, f"{sched} {w}x{h} 8-bit")
+    finally:
+        r.close()
+
+
 def test_band_tiling_partitions_the_frame(gpu):
     sc = pt.cornell_scene(pt.torus_knot(60, 16), cube_length=32)
     cfg = pt.configuration(max_tracer_depth=6)
@@ -347,6 +457,69 @@ def test_reference_abi_path_tracer_kernel(gpu):
     ref, ref8, _ = oracle.render(v, cam, cfg, 1, 3)
     assert_bitwise(got, ref, "ABI float")
     assert_bitwise(got8, ref8, "ABI 8-bit")
+
+
+def _hip_runtime():
+    h = C.CDLL("libamdhip64.so")
+    h.hipMallocManaged.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+    h.hipMallocManaged.restype = C.c_int
+    h.hipFree.argtypes = [C.c_void_p]
+    h.hipFree.restype = C.c_int
+    h.hipDeviceSynchronize.restype = C.c_int
+    return h
+
+
+def test_reference_abi_alternates_with_cpu_twin_on_managed_buffers(require_gpu):
+    """Core/path_tracer.cpp:40-91 picks the GPU entry or the CPU twin path_tracer_cpu per pass, on the
+    SAME managed image (Core/image.cpp:15-27) and scratch (path_tracer_kernel.cu:782-796) buffers. Here
+    passes 1, 3, 4 run through path_tracer_kernel and passes 2, 5 are the CPU twin (the oracle in the
+    reference CPU-fallback mode: MSVC rand, libm) writing the managed buffers on the host. Every GPU
+    pass must add into what the host left there: the result equals the same five-pass chain run by
+    the oracle alone, bit for bit."""
+    sc = pt.cornell_scene(pt.torus_knot(50, 14), cube_length=32)
+    cfg = pt.configuration(max_tracer_depth=5)
+    cam = pt.camera(40, 30, **BENCH_CAM)
+    n = 40 * 30
+    hip = _hip_runtime()
+    lib = pt.lib()
+    pimg, pimg8 = C.c_void_p(), C.c_void_p()
+    assert hip.hipMallocManaged(C.byref(pimg), n * 12, 1) == 0
+    assert hip.hipMallocManaged(C.byref(pimg8), n * 3, 1) == 0
+    scratch = [C.c_void_p() for _ in range(5)]
+    lib.path_tracer_kernel_memory_allocate(*[C.byref(s) for s in scratch], n)
+    try:
+        img = np.ctypeslib.as_array((C.c_float * (n * 3)).from_address(pimg.value))
+        img8 = np.ctypeslib.as_array((C.c_uint8 * (n * 3)).from_address(pimg8.value))
+        img[:] = np.nan  # pass 1 must overwrite whatever the buffers held
+        img8[:] = 7
+        # the scratch is host-accessible, as the CPU twin uses it (path_tracer_cpu.cpp:244-262)
+        for s, nb in zip(scratch, (12, 12, 24, 4, 24)):
+            a = np.ctypeslib.as_array((C.c_uint8 * (n * nb)).from_address(s.value))
+            a[:] = 0xA5
+            assert a[-1] == 0xA5
+        v = sc.view
+        want = np.zeros((n, 3), np.float32)
+        want8 = np.zeros((n, 3), np.uint8)
+        for p, backend in ((1, "gpu"), (2, "cpu"), (3, "gpu"), (4, "gpu"), (5, "cpu")):
+            if backend == "gpu":
+                lib.path_tracer_kernel(v.mesh_num, v.bvh_nodes, v.triangles, v.sphere_num, v.spheres, n,
+                                       C.cast(pimg, C.POINTER(pt._abi.Float3)), C.cast(pimg8, C.POINTER(pt._abi.UChar3)),
+                                       p, C.byref(cam), v.sky_cube_map, *scratch, v.mesh_textures, C.byref(cfg))
+                oracle.render(v, cam, cfg, p, 1, image=want, image256=want8)
+            else:
+                assert hip.hipDeviceSynchronize() == 0
+                oracle.render(v, cam, cfg, p, 1, rng="msvc", math="libm", image=img, image256=img8)
+                oracle.render(v, cam, cfg, p, 1, rng="msvc", math="libm", image=want, image256=want8)
+        assert hip.hipDeviceSynchronize() == 0
+        assert_bitwise(img.reshape(-1, 3), want, "alternating GPU/CPU float")
+        assert_bitwise(img8.reshape(-1, 3), want8, "alternating GPU/CPU 8-bit")
+        # and the chain differs from an all-GPU one (the CPU passes really were picked up)
+        gpu_only, _, _ = oracle.render(v, cam, cfg, 1, 5)
+        assert not np.array_equal(gpu_only, want)
+    finally:
+        lib.path_tracer_kernel_memory_free(*scratch)
+        hip.hipFree(pimg)
+        hip.hipFree(pimg8)
 
 
 def test_reference_abi_sees_in_place_edits(require_gpu):
