@@ -367,7 +367,15 @@ typedef struct {
     or_v3* thr;            /* not_absorbed_colors */
     or_v3* rad;            /* accumulated_colors */
     pt_scattering* sca;    /* scatterings */
+    unsigned long long* sig;  /* optional: per-slot hash of the path's decisions (tolerance calibration) */
 } or_state;
+
+/* Folds one decision of a path into its signature: which primitive the segment hit and which branch of
+ * trace_ray it took. Two renders whose signatures agree took the same path topology, so their radiance
+ * differs only by rounding; a signature that differs is a branch flip (tests/test_oracle.py). */
+static void sig_add(or_state* st, int k, long long code) {
+    if (st->sig) st->sig[k] = (st->sig[k] ^ (unsigned long long)code) * 0x100000001b3ull + 0x9e3779b97f4a7c15ull;
+}
 
 /* init_data (:275-297) + generate_ray (:299-379 | cpu :264-339) for state slot k = pixel */
 static void generate(const or_scene* sc, const pt_render_camera* cam, int rng_kind, int seed, int k, int pixel,
@@ -375,6 +383,7 @@ static void generate(const or_scene* sc, const pt_render_camera* cam, int rng_ki
     const pt_configuration* cfg = sc->cfg;
     int mm = sc->math;
     st->alive[k] = k;
+    if (st->sig) st->sig[k] = 0;
     st->thr[k] = v3(1.0f, 1.0f, 1.0f);
     st->rad[k] = v3(0.0f, 0.0f, 0.0f);
     st->sca[k].absorption_coefficient = cfg->air_absorption_coef;
@@ -447,6 +456,7 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
         float r = draw01(&rng);
         float dist = -m_log(mm, r) / cs.reduced_scattering_coefficient.x;
         if (dist < min_t) {
+            sig_add(st, k, 1);  /* scatter inside the medium */
             float r1 = draw01(&rng), r2 = draw01(&rng);
             st->rays[k].origin = pf3(v_add(o, v_scale(d, dist)));
             st->rays[k].direction = pf3(on_sphere(mm, r1, r2));
@@ -457,6 +467,7 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
         st->thr[k] = v_mul(st->thr[k], absorption_through(mm, cs.absorption_coefficient, min_t));
     }
 
+    sig_add(st, k, 16 + type * 4 + (long long)(type == 1 ? min_sphere : min_tri) * 64);
     if (type == 0) {
         or_v3 bg = background(sc, d);
         st->rad[k] = v_add(st->rad[k], v_mul(st->thr[k], bg));
@@ -511,6 +522,7 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
     else R = fresnel_conductors(min_normal, d, out_n, mat.medium.extinction_coefficient);
 
     float r = draw01(&rng);
+    sig_add(st, k, r < R ? 2 : (mat.is_transparent ? 3 : 4));
     if (r < R) {
         float r1 = draw01(&rng), r2 = draw01(&rng);
         float rough = m_pow(mm, mat.roughness, 1.85f) * 0.238f;
@@ -533,7 +545,7 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
         st->rays[k].origin = pf3(v_add(min_point, bias));
         st->rays[k].direction = pf3(hemisphere_cosine(mm, min_normal, r1, r2));
     }
-    if (v_len(st->thr[k]) <= cfg->energy_exist_threshold) st->alive[ai] = -1;
+    if (v_len(st->thr[k]) <= cfg->energy_exist_threshold) { st->alive[ai] = -1; sig_add(st, k, 5); }
 }
 
 /* thread_shrink: stable remove_if(v < 0) (parallel_function.cu:42-49) */
@@ -562,20 +574,25 @@ static void gamma_u8(int mm, const pt_configuration* cfg, const float* img, int 
  * sum and 8-bit value of entry k, with the reference's pass_counter semantics. stats[0..2] (may be
  * NULL) receive ray segments, BVH nodes visited and triangle tests. Returns 0 or -1 (alloc).
  */
-int or_render(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangle* triangles, int sphere_num,
-              const pt_sphere* spheres, const pt_cube_map* cube, const pt_texture_wrapper* textures,
-              const pt_configuration* cfg, const pt_render_camera* cam, int first_pass, int pass_count,
-              const int* pixel_list, int n, float* image, unsigned char* image256, int rng_kind, int math_mode,
-              int threads, unsigned long long* stats) {
+int or_render_sig(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangle* triangles, int sphere_num,
+                  const pt_sphere* spheres, const pt_cube_map* cube, const pt_texture_wrapper* textures,
+                  const pt_configuration* cfg, const pt_render_camera* cam, int first_pass, int pass_count,
+                  const int* pixel_list, int n, float* image, unsigned char* image256, int rng_kind, int math_mode,
+                  int threads, unsigned long long* stats, unsigned long long* sigs) {
     or_scene sc = {mesh_num, bvh_nodes, triangles, sphere_num, spheres, cube, textures, cfg, math_mode};
     or_state st;
+    st.sig = NULL;
+    if (sigs) {
+        st.sig = (unsigned long long*)malloc((size_t)n * sizeof(unsigned long long));
+        if (!st.sig) return -1;
+    }
     st.alive = (int*)malloc((size_t)n * sizeof(int));
     st.rays = (pt_ray*)malloc((size_t)n * sizeof(pt_ray));
     st.thr = (or_v3*)malloc((size_t)n * sizeof(or_v3));
     st.rad = (or_v3*)malloc((size_t)n * sizeof(or_v3));
     st.sca = (pt_scattering*)malloc((size_t)n * sizeof(pt_scattering));
     if (!st.alive || !st.rays || !st.thr || !st.rad || !st.sca) {
-        free(st.alive); free(st.rays); free(st.thr); free(st.rad); free(st.sca);
+        free(st.alive); free(st.rays); free(st.thr); free(st.rad); free(st.sca); free(st.sig);
         return -1;
     }
 #ifdef _OPENMP
@@ -612,11 +629,21 @@ int or_render(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangle* t
             if (pass != 1) { img[0] = img[0] + c.x; img[1] = img[1] + c.y; img[2] = img[2] + c.z; }
             else { img[0] = c.x; img[1] = c.y; img[2] = c.z; }
             if (image256) gamma_u8(math_mode, cfg, img, pass, image256 + (size_t)k * 3);
+            if (sigs) sigs[(size_t)(pass - first_pass) * n + k] = st.sig[k];
         }
     }
     if (stats) { stats[0] = segs; stats[1] = nodes; stats[2] = tris; }
-    free(st.alive); free(st.rays); free(st.thr); free(st.rad); free(st.sca);
+    free(st.alive); free(st.rays); free(st.thr); free(st.rad); free(st.sca); free(st.sig);
     return 0;
+}
+
+int or_render(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangle* triangles, int sphere_num,
+              const pt_sphere* spheres, const pt_cube_map* cube, const pt_texture_wrapper* textures,
+              const pt_configuration* cfg, const pt_render_camera* cam, int first_pass, int pass_count,
+              const int* pixel_list, int n, float* image, unsigned char* image256, int rng_kind, int math_mode,
+              int threads, unsigned long long* stats) {
+    return or_render_sig(mesh_num, bvh_nodes, triangles, sphere_num, spheres, cube, textures, cfg, cam, first_pass,
+                         pass_count, pixel_list, n, image, image256, rng_kind, math_mode, threads, stats, NULL);
 }
 
 /* The 8-bit gamma output of a float running sum of `pass` passes, for n pixels (used to check the
