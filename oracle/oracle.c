@@ -469,6 +469,12 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
 
     sig_add(st, k, 16 + type * 4 + (long long)(type == 1 ? min_sphere : min_tri) * 64);
     if (type == 0) {
+        if (st->sig) {  /* the sky's cube face: a discontinuity of the background lookup */
+            float u, v;
+            int face;
+            cube_uv(d.x, d.y, d.z, &face, &u, &v);
+            sig_add(st, k, 6 + face * 8);
+        }
         or_v3 bg = background(sc, d);
         st->rad[k] = v_add(st->rad[k], v_mul(st->thr[k], bg));
         st->alive[ai] = -1;

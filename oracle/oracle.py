@@ -14,29 +14,35 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "lib", "liboracle.so")
+# "fma": the same oracle built with FMA contraction (nvcc's default), for the tolerance calibration only
+VARIANTS = {"": LIB, "fma": os.path.join(HERE, "lib", "liboracle_fma.so")}
 
 RNG = {"thrust": 0, "msvc": 1}
 MATH = {"cephes": 0, "libm": 1}
 
-_lib = None
+_libs = {}
 
 
-def build(force: bool = False) -> str:
+def build(force: bool = False, variant: str = "") -> str:
+    path = VARIANTS[variant]
     srcs = [os.path.join(HERE, f) for f in ("oracle.c", "oracle_math.h", "Makefile")]
-    if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
-        subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "lib/liboracle.so"], check=True)
-    return LIB
+    if force or not os.path.exists(path) or any(os.path.getmtime(s) > os.path.getmtime(path) for s in srcs):
+        target = os.path.relpath(path, HERE)
+        subprocess.run(["make", "-s", "-C", HERE] + (["-B"] if force else []) + [target], check=True)
+    return path
 
 
-def lib() -> C.CDLL:
-    global _lib
-    if _lib is None:
-        build()
-        h = C.CDLL(LIB)
+def lib(variant: str = "") -> C.CDLL:
+    if variant not in _libs:
+        build(variant=variant)
+        h = C.CDLL(VARIANTS[variant])
+        args = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         h.or_render.restype = C.c_int
-        h.or_render.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
-                                C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
-                                C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        h.or_render.argtypes = args
+        h.or_render_sig.restype = C.c_int
+        h.or_render_sig.argtypes = args + [C.c_void_p]
         h.or_rng_stream.restype = None
         h.or_rng_stream.argtypes = [C.c_int, C.c_int32, C.c_int, C.c_float, C.c_float, C.c_void_p]
         h.or_hash.restype = C.c_int32
@@ -45,20 +51,24 @@ def lib() -> C.CDLL:
         h.or_gamma_u8.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         h.or_math_eval.restype = None
         h.or_math_eval.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
-        _lib = h
-    return _lib
+        _libs[variant] = h
+    return _libs[variant]
 
 
 def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.ndarray | None = None,
            rng: str = "thrust", math: str = "cephes", threads: int = 0, with_u8: bool = True,
-           image: np.ndarray | None = None, image256: np.ndarray | None = None):
+           image: np.ndarray | None = None, image256: np.ndarray | None = None, variant: str = "",
+           signatures: bool = False):
     """Run passes first_pass..first_pass+pass_count-1 over all pixels (or the given pixel indices).
 
     `image` / `image256` (optional, float32 / uint8, n*3 contiguous) are the caller's running sum and
     8-bit buffers, updated in place with the reference's pass_counter semantics (a pass > 1 adds
     into the running sum): the CPU twin's view of Core/path_tracer.cpp:71-91.
+    `variant` "fma" runs the FMA-contracting build (calibration only). `signatures` adds
+    stats["signatures"]: uint64 [pass_count, n], a hash of each path's decisions (hit primitive and
+    branch per segment): equal signatures = same path topology.
     Returns (image float32 [n,3], image256 uint8 [n,3] or None, stats dict)."""
-    L = lib()
+    L = lib(variant)
     if pixels is None:
         n = int(cam.resolution[0]) * int(cam.resolution[1])
         plist = None
@@ -76,14 +86,19 @@ def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.
     else:
         img8 = np.zeros((n, 3), np.uint8) if with_u8 else None
     stats = (C.c_ulonglong * 3)()
-    rc = L.or_render(view.mesh_num, C.cast(view.bvh_nodes, C.c_void_p), C.cast(view.triangles, C.c_void_p),
+    sigs = np.zeros((pass_count, n), np.uint64) if signatures else None
+    rc = L.or_render_sig(view.mesh_num, C.cast(view.bvh_nodes, C.c_void_p), C.cast(view.triangles, C.c_void_p),
                      view.sphere_num, C.cast(view.spheres, C.c_void_p), C.cast(view.sky_cube_map, C.c_void_p),
                      C.cast(view.mesh_textures, C.c_void_p), C.addressof(cfg), C.addressof(cam), first_pass,
                      pass_count, plist.ctypes.data if plist is not None else None, n, img.ctypes.data,
-                     img8.ctypes.data if img8 is not None else None, RNG[rng], MATH[math], threads, stats)
+                     img8.ctypes.data if img8 is not None else None, RNG[rng], MATH[math], threads, stats,
+                     sigs.ctypes.data if sigs is not None else None)
     if rc != 0:
         raise MemoryError("oracle allocation failed")
-    return img, img8, {"segments": stats[0], "nodes": stats[1], "tris": stats[2]}
+    st = {"segments": stats[0], "nodes": stats[1], "tris": stats[2]}
+    if sigs is not None:
+        st["signatures"] = sigs
+    return img, img8, st
 
 
 def gamma_u8(cfg, image: np.ndarray, pass_: int, math: str = "cephes") -> np.ndarray:

@@ -17,8 +17,11 @@ struct PtMortonTree {
     std::vector<int> inner_parent, leaf_parent;  // -1 = none
 };
 
-// leaf count of bvh.cpp:866-868
+// leaf count of bvh.cpp:866-868. With fewer triangles than a leaf holds the reference's formula gives
+// two leaves, and the second one's first triangle is read past the end of the sorted array (:926-933,
+// undefined; found by the sanitizer build, tests/test_sanitizers.py): here that mesh is one leaf.
 inline unsigned int pt_leaf_count(int n, int leaf_size) {
+    if (n < leaf_size) return 1;
     unsigned int l = (unsigned int)(n / leaf_size);
     l = l == 0 ? 1 : l;
     return (n % leaf_size == 0) ? l : l + 1;

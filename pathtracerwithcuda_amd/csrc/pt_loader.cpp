@@ -256,6 +256,31 @@ pt_material to_material(const Preset& p) {
 }
 
 // ---- OBJ (tinyobjloader 1.1.0 semantics) ---------------------------------------------------------
+// try_parse_double, pnpoly and export_group below follow tinyobjloader 1.1.0 (the OBJ loader the
+// reference vendors, lib/tiny_obj_loader/tiny_obj_loader.h:498-611, :975-1166) closely, because the
+// parsed floats and the triangulation must be bit-identical to it. Its licence:
+//
+//   The MIT License (MIT)
+//
+//   Copyright (c) 2012-2017 Syoyo Fujita and many contributors.
+//
+//   Permission is hereby granted, free of charge, to any person obtaining a copy
+//   of this software and associated documentation files (the "Software"), to deal
+//   in the Software without restriction, including without limitation the rights
+//   to use, copy, modify, merge, publish, distribute, sublicense, and/or sell
+//   copies of the Software, and to permit persons to whom the Software is
+//   furnished to do so, subject to the following conditions:
+//
+//   The above copyright notice and this permission notice shall be included in
+//   all copies or substantial portions of the Software.
+//
+//   THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY KIND, EXPRESS OR
+//   IMPLIED, INCLUDING BUT NOT LIMITED TO THE WARRANTIES OF MERCHANTABILITY,
+//   FITNESS FOR A PARTICULAR PURPOSE AND NONINFRINGEMENT. IN NO EVENT SHALL THE
+//   AUTHORS OR COPYRIGHT HOLDERS BE LIABLE FOR ANY CLAIM, DAMAGES OR OTHER
+//   LIABILITY, WHETHER IN AN ACTION OF CONTRACT, TORT OR OTHERWISE, ARISING FROM,
+//   OUT OF OR IN CONNECTION WITH THE SOFTWARE OR THE USE OR OTHER DEALINGS IN
+//   THE SOFTWARE.
 inline bool is_space(char c) { return c == ' ' || c == '\t'; }
 inline bool is_digit(char c) { return (unsigned)(c - '0') < 10u; }
 inline bool is_new_line(char c) { return c == '\r' || c == '\n' || c == '\0'; }
@@ -369,9 +394,19 @@ int pnpoly(int nvert, const float* vx, const float* vy, float tx, float ty) {
 
 struct ObjShape { std::vector<VIdx> idx; };  // 3 per triangle
 
-// exportFaceGroupToShape with triangulate = true (tiny_obj_loader.h:986-1166)
-bool export_group(ObjShape& shape, std::vector<std::vector<VIdx>>& group, const std::vector<float>& v) {
+// exportFaceGroupToShape with triangulate = true (tiny_obj_loader.h:986-1166). A face naming a vertex
+// that does not exist (yet) sets *bad: tinyobjloader reads past its vertex array there (undefined
+// behaviour, found by the sanitizer build, tests/test_sanitizers.py); this loader rejects the file.
+bool export_group(ObjShape& shape, std::vector<std::vector<VIdx>>& group, const std::vector<float>& v,
+                  bool* bad = nullptr) {
     if (group.empty()) return false;
+    const long long nv = (long long)(v.size() / 3);
+    for (const auto& face : group)
+        for (const VIdx& c : face)
+            if (c.v < 0 || c.v >= nv) {
+                if (bad) *bad = true;
+                return false;
+            }
     for (const auto& face : group) {
         size_t npolys = face.size();
         if (npolys < 3) {  // the reference reads face[1] and walks (k+2)%npolys; a degenerate face emits nothing
@@ -517,7 +552,9 @@ bool load_obj_file(const std::string& path, std::vector<float>& v, std::vector<f
             auto it = material_map.find(name);
             if (it != material_map.end()) id = it->second;
             if (id != material) {
-                export_group(shape, group, v);
+                bool bad = false;
+                export_group(shape, group, v, &bad);
+                if (bad) { err = "face index out of range"; return false; }
                 group.clear();
                 material = id;
             }
@@ -534,7 +571,9 @@ bool load_obj_file(const std::string& path, std::vector<float>& v, std::vector<f
             continue;
         }
         if (token[0] == 'g' && is_space(token[1])) {
-            export_group(shape, group, v);
+            bool bad = false;
+            export_group(shape, group, v, &bad);
+            if (bad) { err = "face index out of range"; return false; }
             if (!shape.idx.empty()) shapes.push_back(shape);
             shape = ObjShape();
             group.clear();
@@ -543,13 +582,17 @@ bool load_obj_file(const std::string& path, std::vector<float>& v, std::vector<f
         if (token[0] == 'o' && is_space(token[1])) {
             // the face group is flushed, but the shape is kept only if that flush exported faces
             // (tiny_obj_loader.h:1886-1905)
-            if (export_group(shape, group, v)) shapes.push_back(shape);
+            bool bad = false;
+            if (export_group(shape, group, v, &bad)) shapes.push_back(shape);
+            if (bad) { err = "face index out of range"; return false; }
             group.clear();
             shape = ObjShape();
             continue;
         }
     }
-    const bool ret = export_group(shape, group, v);
+    bool bad = false;
+    const bool ret = export_group(shape, group, v, &bad);
+    if (bad) { err = "face index out of range"; return false; }
     if (ret || !shape.idx.empty()) shapes.push_back(shape);
     return true;
 }

@@ -48,7 +48,9 @@ def build_py(tris, start, leaf_size):
         return morton_py(p)
 
     order = sorted(range(n), key=lambda i: code(boxes[i]))  # stable
-    L = max(n // leaf_size, 1) + (0 if n % leaf_size == 0 else 1)
+    # bvh.cpp:866-868, except a mesh smaller than one leaf is one leaf (the reference reads past the
+    # sorted array there; pt_bvh_internal.h pt_leaf_count)
+    L = 1 if n < leaf_size else max(n // leaf_size, 1) + (0 if n % leaf_size == 0 else 1)
     leaves = []
     for i in range(L):
         s = i * leaf_size

@@ -105,13 +105,38 @@ def test_oracle_pass_accumulation_and_threads(small_scene):
     assert np.array_equal(a, (p1 + p2) + p3)
 
 
-def test_libm_mode_is_close_to_cephes(small_scene):
-    """Calibrates the float tolerance: swapping every transcendental for glibc's (1-ulp scale changes,
-    the same order as the reference's CUDA intrinsics) moves few pixels and the image mean barely."""
-    cfg = pt.configuration(max_tracer_depth=6)
-    cam = pt.camera(64, 48, pitch=0.08, radius=12.5, center=(0, 1.2, 0))
-    a, _, _ = oracle.render(small_scene.view, cam, cfg, 1, 4)
-    b, _, _ = oracle.render(small_scene.view, cam, cfg, 1, 4, math="libm")
-    d = np.abs(a - b)
-    assert (d.max(axis=1) <= 1e-3).mean() >= 0.97
-    assert abs(a.mean() - b.mean()) <= 0.02 * a.mean()
+@pytest.fixture(scope="module")
+def metric_subset():
+    """BASELINE.json's metric frame (1920x1080, 70k-triangle knot, depth 8, 8 passes) on a 20,000-pixel
+    subset, rendered by the bit-exact restatement (Cephes transcendentals, no contraction)."""
+    import bench
+    wl = bench.Workload("metric")
+    sel = np.sort(np.random.default_rng(1).choice(wl.width * wl.height, 20000, replace=False)).astype(np.int32)
+    a, _, sa = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, 8, pixels=sel, signatures=True)
+    return wl, sel, a, sa["signatures"]
+
+
+@pytest.mark.parametrize("model", ["libm", "fma", "fma+libm"])
+def test_tolerance_to_a_cuda_like_build(metric_subset, model):
+    """The stated per-pixel tolerance against the reference CUDA renderer. The CUDA build
+    cannot run here; what separates it from this bit-exact restatement is (a) its hardware intrinsics
+    for sin/cos/exp/log/pow (path_tracer_kernel.cu:191,203-204,235,245-247,464,571,595,660-662) and
+    (b) nvcc's default FMA contraction. Both are modelled on the same frame: glibc's transcendentals
+    ("libm"), the oracle compiled with -ffp-contract=fast ("fma"), and both. Measured (20,000 pixels,
+    8 passes): 99.98-99.995 % of pixels within 1e-3 per channel of the 8-pass running sum, RMSE
+    1.8-3.3e-4 x the mean, |mean shift| < 2e-6, 1.0-5.6e-4 of the (pixel, pass) paths change topology
+    (hit primitive, branch, sky face), and all but at most 2 pixels beyond 1e-3 contain such a flip.
+    The test holds the stated bounds: >= 99.9 % within 1e-3, RMSE <= 1e-3 x mean, |mean shift| <= 1e-5,
+    no NaN/Inf, flips in <= 1 % of pixels, <= 5 diverged pixels without a flip."""
+    wl, sel, a, sig_a = metric_subset
+    kw = {"libm": dict(math="libm"), "fma": dict(variant="fma"), "fma+libm": dict(variant="fma", math="libm")}[model]
+    b, _, sb = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, 8, pixels=sel, signatures=True, **kw)
+    assert np.isfinite(b).all() and np.isfinite(a).all()
+    d = np.abs(a.astype(np.float64) - b).max(axis=1)
+    flipped = (sig_a != sb["signatures"]).any(axis=0)
+    assert (d <= 1e-3).mean() >= 0.999
+    assert np.sqrt(np.mean((a.astype(np.float64) - b) ** 2)) <= 1e-3 * a.mean()
+    assert abs(float(b.mean()) - float(a.mean())) <= 1e-5 * float(a.mean())
+    assert flipped.mean() <= 0.01
+    assert ((d > 1e-3) & ~flipped).sum() <= 5
+    assert flipped.any()  # the models do perturb the paths (the test is not vacuous)

@@ -31,7 +31,7 @@ def main():
     subprocess.run(["gcc", "-O2", "-std=gnu11", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fopenmp",
                     "-shared", os.path.join(ROOT, "tools", "traversal_study.c"), "-o", so, "-lm"], check=True)
     oracle.build()
-    oracle.LIB = so
+    oracle.VARIANTS[""] = so
     L = oracle.lib()
     L.study_stats.argtypes = [C.c_void_p]
     scene = pt.cornell_scene(pt.torus_knot(*bench.KNOT))
