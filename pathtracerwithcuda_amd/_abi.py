@@ -189,6 +189,8 @@ _PROTOS = {
                                   C.c_int, C.c_int, C.POINTER(Sphere), C.POINTER(CubeMap), C.POINTER(TextureWrapper),
                                   C.c_int, C.POINTER(Configuration)]),
     "pt_scene_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong), c_int_p, c_int_p]),
+    "pt_scene_walk_info": (C.c_int, [C.c_void_p, c_int_p, c_int_p]),
+    "pt_set_wide_walk": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_frame_setup": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "pt_set_tiling": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
     "pt_render_passes": (C.c_int, [C.c_void_p, C.POINTER(RenderCamera), C.POINTER(Configuration), C.c_int, C.c_int,

@@ -178,13 +178,23 @@ enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3, LANE_T
 
 // Starts the walk of the first mesh at or after `mesh` with a non-empty node range. The ranges of the
 // first PT_LDS_MESHES meshes come from the workgroup's LDS copy (lds_mesh, filled at kernel start), the
-// rest from global memory.
+// rest from global memory. `wide`: the lane walks the wide records (pt_path.h walk_wide): its position is
+// the mesh's wide start (lds_wroot / mesh_wide) and `end` is -1, the wide walk's end marker.
 #define PT_LDS_MESHES 64
 typedef int i32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ bool start_mesh(const DevScene& sc, const int2* lds_mesh, int& mesh, MeshWalk& w) {
+__device__ __forceinline__ bool start_mesh(const DevScene& sc, const int2* lds_mesh, const int* lds_wroot, bool wide,
+                                           int& mesh, MeshWalk& w) {
     while (mesh < sc.mesh_num) {
         int2 r;
-        if (mesh < PT_LDS_MESHES) {
+        if (wide) {
+            int root;
+            if (mesh < PT_LDS_MESHES) {
+                root = lds_wroot[mesh];
+            } else {
+                root = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(sc.mesh_wide, sc.mesh_num * 4), mesh * 4, 0, 0);
+            }
+            r.x = root; r.y = root == -1 ? -1 : -2;  // -1: empty mesh
+        } else if (mesh < PT_LDS_MESHES) {
             r = lds_mesh[mesh];
         } else {  // a buffer load (not a pointer select that would turn both into flat loads)
             const i32x2 v = __builtin_bit_cast(i32x2, __builtin_amdgcn_raw_buffer_load_b64(
@@ -192,7 +202,7 @@ __device__ __forceinline__ bool start_mesh(const DevScene& sc, const int2* lds_m
             r.x = v.x; r.y = v.y;
         }
         if (r.x != r.y) {
-            w.pos = r.x; w.end = r.y;
+            w.pos = r.x; w.end = wide ? -1 : r.y;
             w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
             return true;
         }
@@ -202,7 +212,9 @@ __device__ __forceinline__ bool start_mesh(const DevScene& sc, const int2* lds_m
 }
 
 // Start of one trace_ray_kernel invocation (path_tracer_kernel.cu:418-454): brute-force spheres into
-// the closest hit, then the walk of mesh 0.
+// the closest hit, then the walk of mesh 0. WIDE scenes: a lane whose 1/d is finite walks the wide
+// records, any other the binary nodes (walk_wide's exactness needs a finite 1/d).
+template <bool WIDE>
 __device__ __forceinline__ int begin_segment(const DevScene& sc, const int2* lds_mesh, const PathState& ps, v3& inv,
                                              Hit& h, MeshWalk& w, int& mesh) {
     h.t = __builtin_inff(); h.t1 = __builtin_inff(); h.t2 = __builtin_inff();
@@ -216,7 +228,12 @@ __device__ __forceinline__ int begin_segment(const DevScene& sc, const int2* lds
     if (sc.first_mesh >= sc.mesh_num) return LANE_READY;  // (start_mesh from mesh 0, resolved on the host)
     inv = mk3(rcp_exact(ps.d.x), rcp_exact(ps.d.y), rcp_exact(ps.d.z));  // == 1.0f / d
     mesh = sc.first_mesh;
-    w.pos = sc.first_range.x; w.end = sc.first_range.y;
+    const bool wide = WIDE && __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
+    if (wide) {
+        w.pos = sc.first_wide; w.end = -1;
+    } else {
+        w.pos = sc.first_range.x; w.end = sc.first_range.y;
+    }
     w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
     return LANE_WALK;
 }
@@ -243,7 +260,7 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
 // PROF: wave-level occupancy counters of the state machine into stats[16..23] (tools/uprof.py):
 // rounds, walk steps, walking lanes summed over steps, shading batches, lanes shaded, triangle
 // batches, lanes in triangle batches, lanes refilled.
-template <int MINW, bool PROF, bool QN, int CHAIN, bool PF>
+template <int MINW, bool PROF, bool QN, int CHAIN, bool PF, bool WIDE>
 __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
                                                                 int walk_steps, int tri_min, int walk_min, int tail) {
@@ -253,12 +270,17 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     // workgroup copies in LDS: the first mesh ranges, every material and every sphere (the launch
     // reserves their bytes of dynamic LDS; pass_kernel_u runs only when that fits, PT_LDS_TABLES)
     __shared__ int2 lds_mesh[PT_LDS_MESHES];
+    __shared__ int lds_wroot[WIDE ? PT_LDS_MESHES : 1];
     extern __shared__ float4 lds_dyn[];
     DevMaterial* lds_mats = reinterpret_cast<DevMaterial*>(lds_dyn);
     {
         const int2* mr = uniform_ptr(P0->sc.mesh_range);
         const int n = min(uniform_int(P0->sc.mesh_num), PT_LDS_MESHES);
         for (int i = threadIdx.x; i < n; i += PT_UBLOCK) lds_mesh[i] = mr[i];
+        if (WIDE) {
+            const int* mw = uniform_ptr(P0->sc.mesh_wide);
+            for (int i = threadIdx.x; i < n; i += PT_UBLOCK) lds_wroot[i] = mw[i];
+        }
         const float4* ms = reinterpret_cast<const float4*>(uniform_ptr(P0->sc.materials));
         const int nm = uniform_int(P0->sc.material_num) * (int)(sizeof(DevMaterial) / 16);
         for (int i = threadIdx.x; i < nm; i += PT_UBLOCK) lds_dyn[i] = ms[i];
@@ -322,7 +344,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     pseed = path_seed(hseed, pixel);
                     depth = 0;
                     if (cfg.max_depth > 0) {
-                        mode = begin_segment(sc, lds_mesh, ps, inv, h, w, mesh);
+                        mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
                     } else {
                         finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
                     }
@@ -361,7 +383,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
                     mode = LANE_WANT;
                 } else {
-                    mode = begin_segment(sc, lds_mesh, ps, inv, h, w, mesh);
+                    mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
                 }
             }
             if (PROF) prof[15] += __builtin_readcyclecounter() - tc2;
@@ -371,6 +393,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
 
         const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
         const __amdgpu_buffer_rsrc_t rt = make_rsrc(sc.tri_geom, sc.tri_count * 48);
+        const __amdgpu_buffer_rsrc_t rw = WIDE ? make_rsrc(sc.wide, sc.wide_count * 128) : rn;
         __amdgpu_buffer_rsrc_t rq = rn;
         float4 fb = make_float4(0.0f, 0.0f, 0.0f, 0.0f), fs = fb;
         if (QN) {
@@ -384,7 +407,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 h.t = w.t; h.t1 = w.t1; h.t2 = w.t2; h.prim = w.tri; h.type = 2;
             }
             mesh++;
-            mode = start_mesh(sc, lds_mesh, mesh, w) ? LANE_WALK : LANE_READY;
+            mode = start_mesh(sc, lds_mesh, lds_wroot, WIDE && w.end < 0, mesh, w) ? LANE_WALK : LANE_READY;
         };
         // PF: the parked triangle's geometry, loaded at the park; scoped to the walk loop, which no lane
         // leaves parked (the last step flushes the batch), so it is not live across shading
@@ -399,8 +422,10 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     bool l2 = walk_box(rn, o2, i2, w2, t2);
                     opaque(w2); opaque(l2); opaque(t2);
                 }
-                const bool leaf = QN ? walk_box_q(rq, fb, fs, ps.o, inv, w, ptri)
-                                     : (CHAIN > 1 ? walk_box_chain<CHAIN>(rn, ps.o, inv, w, ptri) : walk_box(rn, ps.o, inv, w, ptri));
+                bool leaf;
+                if (WIDE && w.end < 0) leaf = walk_wide(rw, ps.o, inv, w, ptri);
+                else leaf = QN ? walk_box_q(rq, fb, fs, ps.o, inv, w, ptri)
+                               : (CHAIN > 1 ? walk_box_chain<CHAIN>(rn, ps.o, inv, w, ptri) : walk_box(rn, ps.o, inv, w, ptri));
                 if (leaf) {
                     mode = LANE_TRI;
                     if (PF && !QN) {  // the triangle's loads are in flight while the batch fills
@@ -426,8 +451,9 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                             walk_tri(rt, o2, d2, w2, t2);
                             opaque(w2);
                         }
-                        if (PF) walk_tri_geom(pta, ptb, ptc, ps.o, ps.d, w, ptri);
-                        else walk_tri(rt, ps.o, ps.d, w, ptri);
+                        const bool advance = !(WIDE && w.end < 0);  // walk_wide already moved past the leaf
+                        if (PF) walk_tri_geom(pta, ptb, ptc, ps.o, ps.d, w, ptri, advance);
+                        else walk_tri(rt, ps.o, ps.d, w, ptri, advance);
                     }
                     mode = LANE_WALK;
                     if (w.pos == w.end) mesh_done();
@@ -638,18 +664,21 @@ bool unified_enabled() {
 
 using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int, int, int);
 
-// PT_WALK_CHAIN: records per walk step (walk_box_chain); 1 = walk_box.
-static PassFnU pass_fn_u(int minw, bool qn) {
+// PT_WALK_CHAIN: records per binary walk step (walk_box_chain); 1 = walk_box. wide: the scene has wide
+// records and PT_WIDE (default 1) allows their walk (walk_wide).
+static PassFnU pass_fn_u(int minw, bool qn, bool wide) {
     static const int prof = env_int("PT_UPROF", 0, 0, 1);
     static const int chain = env_int("PT_WALK_CHAIN", 2, 1, 3);
     static const int pf = env_int("PT_TRI_PREFETCH", 1, 0, 1);
-    if (prof) return qn ? pass_kernel_u<6, true, true, 1, false> : pass_kernel_u<6, true, false, 2, true>;
-    if (qn) return minw == 6 ? pass_kernel_u<6, false, true, 1, false> : pass_kernel_u<5, false, true, 1, false>;
-    if (chain == 1) return minw == 6 ? pass_kernel_u<6, false, false, 1, false> : pass_kernel_u<5, false, false, 1, false>;
-    if (chain == 3) return minw == 6 ? pass_kernel_u<6, false, false, 3, false> : pass_kernel_u<5, false, false, 3, false>;
-    if (pf) return minw == 7 ? pass_kernel_u<7, false, false, 2, true>
-                             : (minw == 6 ? pass_kernel_u<6, false, false, 2, true> : pass_kernel_u<5, false, false, 2, true>);
-    return minw == 6 ? pass_kernel_u<6, false, false, 2, false> : pass_kernel_u<5, false, false, 2, false>;
+    if (prof) return qn ? pass_kernel_u<6, true, true, 1, false, false>
+                        : (wide ? pass_kernel_u<6, true, false, 2, true, true> : pass_kernel_u<6, true, false, 2, true, false>);
+    if (qn) return minw == 6 ? pass_kernel_u<6, false, true, 1, false, false> : pass_kernel_u<5, false, true, 1, false, false>;
+    if (wide) return minw == 5 ? pass_kernel_u<5, false, false, 2, true, true> : pass_kernel_u<6, false, false, 2, true, true>;
+    if (chain == 1) return minw == 6 ? pass_kernel_u<6, false, false, 1, false, false> : pass_kernel_u<5, false, false, 1, false, false>;
+    if (chain == 3) return minw == 6 ? pass_kernel_u<6, false, false, 3, false, false> : pass_kernel_u<5, false, false, 3, false, false>;
+    if (pf) return minw == 7 ? pass_kernel_u<7, false, false, 2, true, false>
+                             : (minw == 6 ? pass_kernel_u<6, false, false, 2, true, false> : pass_kernel_u<5, false, false, 2, true, false>);
+    return minw == 6 ? pass_kernel_u<6, false, false, 2, false, false> : pass_kernel_u<5, false, false, 2, false, false>;
 }
 
 // pass_kernel_u keeps every material and sphere in LDS: scenes whose tables exceed PT_LDS_TABLES bytes
@@ -660,7 +689,7 @@ static bool use_unified(bool leaf1, bool stats, bool qn, int lds_bytes) {
     return leaf1 && !stats && unified_enabled() && lds_bytes <= PT_LDS_TABLES;
 }
 
-hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int first_pass, int batch_log2,
+hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, bool wide, int first_pass, int batch_log2,
                        int write_u8, int grid, bool stats, int lds_bytes, hipStream_t stream) {
     if (use_unified(leaf1, stats, qn, lds_bytes)) {
         // 64-unit chunks and a 28-lane shading batch: measured best with frames in flight
@@ -676,7 +705,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, int 
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
             a8 = walk_min, a9 = tail_shade | (tail_walk << 8);
         void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8, &a9};
-        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn), dim3(grid), dim3(PT_UBLOCK), args,
+        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn, wide && !qn), dim3(grid), dim3(PT_UBLOCK), args,
                                        (size_t)lds_bytes, stream);
         if (e != hipSuccess) return e;
         return hipGetLastError();
@@ -707,12 +736,12 @@ hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256
     return hipGetLastError();
 }
 
-int pass_grid_size(bool leaf1, bool stats, bool qn, int lds_bytes) {
+int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int lds_bytes) {
     int dev = 0, cus = 0, blocks = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const bool u = use_unified(leaf1, stats, qn, lds_bytes);
-    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true), qn)
+    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true), qn, wide && !qn)
                        : (const void*)pass_fn(leaf1, stats, pass_min_waves(false), qn);
     const size_t lds = u ? (size_t)lds_bytes : 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, u ? PT_UBLOCK : PT_BLOCK, lds) != hipSuccess || blocks <= 0) blocks = u ? 4 * PT_BLOCK / PT_UBLOCK : 4;

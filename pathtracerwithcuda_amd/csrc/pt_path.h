@@ -512,22 +512,88 @@ __device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, 
     return chain_test<CHAIN>(r, o, inv, w, tri);
 }
 
-// walk_tri with the triangle's records already loaded.
-__device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri) {
+// ---- the wide walk (pt_scene.h `wide`, built by pt_runtime.cpp build_wide) ------------------------
+// One step loads a wide record — up to four binary nodes that follow each other in the binary preorder
+// once the levels between them are collapsed — and takes, from the walk's slot on, the first node whose
+// box passes the reference's test (bounding_box.h:83-102 and `entry <= min_t`, path_tracer_kernel.cu:
+// 113-150): an internal node is descended (its record is the next step), a leaf parks the lane for its
+// triangle with the position after it. No passing slot: the record's skip position.
+//
+// Exactness. The reference also tests the collapsed binary nodes; this walk does not. Every box
+// contains its children's boxes (checked on the host), the slab arithmetic (lo - o) * inv, min, max
+// is monotone in the box planes when inv is finite (no 0 * inf), and min_t only decreases: so a node
+// whose test passes would have had every ancestor pass when the reference tested it, with a min_t at
+// least as large. The walk therefore reaches exactly the leaves whose own test passes, in the same
+// preorder, and tests their triangles under the same min_t: the same accepted hits as the reference.
+// A ray with an infinite 1/d (a zero direction component) can produce NaN slabs, for which the
+// argument fails; such lanes walk the binary nodes (pass_kernel_u, begin_segment).
+__device__ __forceinline__ float sel4(float4 v, int j) { return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w)); }
+
+__device__ __forceinline__ bool box_hit_s(float lx, float ly, float lz, float hx, float hy, float hz, v3 o, v3 inv,
+                                          float* entry) {
+    float tx1 = (lx - o.x) * inv.x;
+    float tx2 = (hx - o.x) * inv.x;
+    float ty1 = (ly - o.y) * inv.y;
+    float ty2 = (hy - o.y) * inv.y;
+    float tz1 = (lz - o.z) * inv.z;
+    float tz2 = (hz - o.z) * inv.z;
+    float t_max = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    float t_min = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    *entry = t_max;
+    return t_max <= t_min && t_min > 0.0f;
+}
+
+__device__ __forceinline__ bool walk_wide(const __amdgpu_buffer_rsrc_t rw, v3 o, v3 inv, MeshWalk& w, int& tri) {
+    const int rec = w.pos >> 2, k = w.pos & 3;
+    float4 r[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) r[i] = bload(rw, rec * 128 + 16 * i);
+    // all eight loads issued before the first test (one round trip per step)
+#pragma unroll
+    for (int i = 1; i < 8; i++) asm volatile("" ::"v"(r[i].x), "v"(r[i].w));
+    const int skip = f2i(r[7].x), n = f2i(r[7].y);
+    unsigned int pass = 0;
+#pragma unroll
+    for (int j = 0; j < PT_WIDE_SLOTS; j++) {
+        float entry;
+        const bool h = box_hit_s(sel4(r[0], j), sel4(r[2], j), sel4(r[4], j), sel4(r[1], j), sel4(r[3], j),
+                                 sel4(r[5], j), o, inv, &entry);
+        if (h && entry <= w.t && j >= k && j < n) pass |= 1u << j;
+    }
+    if (pass == 0) {
+        w.pos = skip;
+        return false;
+    }
+    const int j = __builtin_ctz(pass);
+    const int ref = f2i(sel4(r[6], j));
+    if (ref > 0) {  // internal: its record is the next step
+        w.pos = ref << 2;
+        return false;
+    }
+    tri = -ref - 1;  // leaf: its triangle, then the next slot (or the skip after the last one)
+    w.pos = j + 1 < n ? ((rec << 2) | (j + 1)) : skip;
+    return true;
+}
+
+// walk_tri with the triangle's records already loaded. `advance`: the binary walk moves to pos + 1
+// after the leaf; the wide walk already holds the position after it (walk_wide).
+__device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri,
+                                              bool advance = true) {
     float t, t1, t2;
     if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t) {
         w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
     }
-    w.pos++;
+    if (advance) w.pos++;
 }
 
-__device__ __forceinline__ void walk_tri(const __amdgpu_buffer_rsrc_t rt, v3 o, v3 d, MeshWalk& w, int tri) {
+__device__ __forceinline__ void walk_tri(const __amdgpu_buffer_rsrc_t rt, v3 o, v3 d, MeshWalk& w, int tri,
+                                         bool advance = true) {
     float t, t1, t2;
     const float4 a = bload(rt, tri * 48), b = bload(rt, tri * 48 + 16), c = bload(rt, tri * 48 + 32);
     if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t) {
         w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
     }
-    w.pos++;
+    if (advance) w.pos++;
 }
 
 // The same two stages on the 16-B quantised nodes (mesh_closest_q's rules) with the scene-wide frame

@@ -56,6 +56,8 @@ struct SceneStage {
     std::vector<float4> nodes;
     std::vector<uint4> qnodes;     // empty: quantised walk unavailable (leaf size > 1, odd input)
     std::vector<float4> mesh_q;
+    std::vector<float4> wide;      // empty: wide walk unavailable (leaf size > 1, a box not inside its parent's)
+    std::vector<int> mesh_wide;    // per mesh: the wide walk's start position, or -1 (no nodes)
     std::vector<int> leaf_tris;
     std::vector<int2> mesh_range;
     std::vector<float4> tri_geom, tri_shade, spheres;
@@ -181,6 +183,122 @@ void quantise_nodes(SceneStage& st) {
         }
     }
     st.qnodes.swap(q);
+}
+
+// Wide records (pt_scene.h `wide`, pt_path.h walk_wide) from the binary preorder nodes of st.nodes, leaf
+// size 1. A wide node stands for a binary internal node B: its slots are B's children, the internal one
+// with the largest box area replaced by its own two children (in place, so the slots stay in the
+// binary preorder) until there are PT_WIDE_SLOTS of them. The walk over them visits the binary
+// preorder without the collapsed levels, which is exact because every box contains its children's
+// (checked here for every parent/child pair; the scene gets no wide records otherwise): see walk_wide.
+void build_wide(SceneStage& st) {
+    st.wide.clear();
+    st.mesh_wide.clear();
+    if (st.leaf_size != 1) return;
+    const int N = (int)(st.nodes.size() / 2);
+    auto lo = [&](int i) { return st.nodes[2 * (size_t)i]; };
+    auto hi = [&](int i) { return st.nodes[2 * (size_t)i + 1]; };
+    auto is_leaf = [&](int i) { return f2i_host(hi(i).w) >= 0; };
+    auto inside = [&](int c, int p) {
+        const float4 a = lo(c), b = hi(c), pa = lo(p), pb = hi(p);
+        return a.x >= pa.x && a.y >= pa.y && a.z >= pa.z && b.x <= pb.x && b.y <= pb.y && b.z <= pb.z;
+    };
+    for (int i = 0; i < N; i++) {  // finite, bounded coordinates: no inf - inf or overflow in (lo - o) * inv
+        const float v[6] = {lo(i).x, lo(i).y, lo(i).z, hi(i).x, hi(i).y, hi(i).z};
+        for (float x : v)
+            if (!(std::fabs(x) < 1e30f)) return;
+    }
+    struct WRec { int n; int bin[PT_WIDE_SLOTS]; int ref[PT_WIDE_SLOTS]; int skip; };
+    std::vector<WRec> recs;
+    std::vector<int> mesh_root;
+    for (const int2& r : st.mesh_range) {
+        if (r.x == r.y) { mesh_root.push_back(-1); continue; }
+        // children of internal node i: i + 1 and the left child's skip index
+        auto left = [&](int i) { return i + 1; };
+        auto right = [&](int i) { return f2i_host(lo(i + 1).w); };
+        for (int i = r.x; i < r.y; i++) {
+            if (is_leaf(i)) {
+                if (f2i_host(lo(i).w) != i + 1) return;
+            } else {
+                if (i + 1 >= r.y || right(i) <= i + 1 || right(i) >= r.y) return;
+                if (!inside(left(i), i) || !inside(right(i), i)) return;
+            }
+        }
+        const int root_id = (int)recs.size();
+        mesh_root.push_back(root_id << 2);
+        // depth-first, numbering a wide node when it is entered: ids in the walk's preorder (a parent
+        // before its children, siblings in slot order)
+        struct Todo { int bin, parent, slot; };
+        std::vector<Todo> todo{{r.x, -1, 0}};
+        while (!todo.empty()) {
+            const Todo t = todo.back();
+            todo.pop_back();
+            const int id = (int)recs.size();
+            recs.push_back(WRec{});
+            if (t.parent >= 0) recs[t.parent].ref[t.slot] = id;
+            const int b = t.bin;
+            int list[PT_WIDE_SLOTS], n = 0;
+            if (is_leaf(b)) {
+                list[n++] = b;  // a one-leaf mesh: its root is the only slot
+            } else {
+                list[n++] = left(b);
+                list[n++] = right(b);
+                while (n < PT_WIDE_SLOTS) {
+                    int best = -1;
+                    float ba = -1.0f;
+                    for (int q = 0; q < n; q++) {
+                        if (is_leaf(list[q])) continue;
+                        const float dx = hi(list[q]).x - lo(list[q]).x, dy = hi(list[q]).y - lo(list[q]).y,
+                                    dz = hi(list[q]).z - lo(list[q]).z;
+                        const float a = dx * dy + dy * dz + dz * dx;
+                        if (a > ba) { ba = a; best = q; }
+                    }
+                    if (best < 0) break;
+                    const int c = list[best];
+                    for (int q = n; q > best + 1; q--) list[q] = list[q - 1];
+                    list[best] = left(c);
+                    list[best + 1] = right(c);
+                    n++;
+                }
+            }
+            recs[id].n = n;
+            for (int q = 0; q < n; q++) {
+                recs[id].bin[q] = list[q];
+                recs[id].ref[q] = is_leaf(list[q]) ? -(f2i_host(hi(list[q]).w) + 1) : 0;
+            }
+            for (int q = n - 1; q >= 0; q--)
+                if (!is_leaf(list[q])) todo.push_back({list[q], id, q});
+        }
+        // skips: after a wide node's subtree, the next slot of its parent, or the parent's own skip
+        recs[root_id].skip = -1;
+        for (int id = root_id; id < (int)recs.size(); id++)
+            for (int s = 0; s < recs[id].n; s++) {
+                const int c = recs[id].ref[s];
+                if (c < 0) continue;
+                recs[c].skip = s + 1 < recs[id].n ? ((id << 2) | (s + 1)) : recs[id].skip;
+            }
+    }
+    // a parent is numbered before its children, so the forward loop above saw every parent's skip first
+    for (size_t id = 0; id < recs.size(); id++)
+        for (int s = 0; s < recs[id].n; s++)
+            if (recs[id].ref[s] >= 0 && recs[id].ref[s] <= (int)id) return;  // not a preorder numbering
+    std::vector<float4> w(recs.size() * 8);
+    for (size_t id = 0; id < recs.size(); id++) {
+        const WRec& R = recs[id];
+        float c[6][PT_WIDE_SLOTS];
+        int ref[PT_WIDE_SLOTS];
+        for (int s = 0; s < PT_WIDE_SLOTS; s++) {
+            const bool used = s < R.n;
+            const float4 a = used ? lo(R.bin[s]) : mkf4(0, 0, 0, 0), b = used ? hi(R.bin[s]) : mkf4(0, 0, 0, 0);
+            c[0][s] = a.x; c[1][s] = b.x; c[2][s] = a.y; c[3][s] = b.y; c[4][s] = a.z; c[5][s] = b.z;
+            ref[s] = used ? R.ref[s] : 0;
+        }
+        for (int k = 0; k < 6; k++) w[id * 8 + k] = mkf4(c[k][0], c[k][1], c[k][2], c[k][3]);
+        w[id * 8 + 6] = mkf4(i2f(ref[0]), i2f(ref[1]), i2f(ref[2]), i2f(ref[3]));
+        w[id * 8 + 7] = mkf4(i2f(R.skip), i2f(R.n), 0.0f, 0.0f);
+    }
+    st.wide.swap(w);
+    st.mesh_wide.swap(mesh_root);
 }
 
 // Reference layout -> device layout (pt_scene.h). Reads every embedded pointer on the host.
@@ -325,7 +443,7 @@ struct pt_context {
     void* scene_mem = nullptr;
     size_t scene_bytes = 0;
     DevScene scene{};
-    int node_num = 0, tri_num = 0;
+    int node_num = 0, tri_num = 0, wide_num = 0;
     bool has_scene = false;
     int material_num = 0;
     float mat_air_n = 0.0f;       // air index the per-material constants were computed for
@@ -343,7 +461,8 @@ struct pt_context {
     LaunchParams* params = nullptr;  // device copy of the launch parameter block
     bool instrumented = false;
     int schedule = -1;  // PT_SCHEDULE_*; -1: environment default (PT_MODE)
-    int grid[2][2][2] = {};
+    int wide_mode = -1; // pass_kernel_u walks the wide records: 1 on, 0 off, -1 environment default (PT_WIDE)
+    int grid[2][2][3] = {};
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
     size_t ev_used = 0;
@@ -406,6 +525,8 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     size_t i_cube = add(st.cube.data(), st.cube.size());
     size_t i_q = add(st.qnodes.data(), st.qnodes.size() * sizeof(uint4));
     size_t i_mq = add(st.mesh_q.data(), st.mesh_q.size() * sizeof(float4));
+    size_t i_w = add(st.wide.data(), st.wide.size() * sizeof(float4));
+    size_t i_mw = add(st.mesh_wide.data(), st.mesh_wide.size() * sizeof(int));
     free_scene(ctx);
     if (total == 0) total = 256;
     PT_HIP(hipMalloc(&ctx->scene_mem, total));
@@ -427,6 +548,9 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     s.cube = (const uint8_t*)(base + pieces[i_cube].off);
     s.qnodes = st.qnodes.empty() ? nullptr : (const uint4*)(base + pieces[i_q].off);
     s.mesh_q = st.mesh_q.empty() ? nullptr : (const float4*)(base + pieces[i_mq].off);
+    s.wide = st.wide.empty() ? nullptr : (const float4*)(base + pieces[i_w].off);
+    s.mesh_wide = st.wide.empty() ? nullptr : (const int*)(base + pieces[i_mw].off);
+    s.wide_count = (int)(st.wide.size() / 8);
     s.mesh_num = (int)st.mesh_range.size();
     s.sphere_num = (int)(st.spheres.size() / 2);
     s.leaf_size = st.leaf_size;
@@ -436,13 +560,16 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     s.material_num = (int)st.mats.size();
     s.first_mesh = (int)st.mesh_range.size();
     s.first_range = int2{0, 0};
+    s.first_wide = -1;
     for (size_t m = 0; m < st.mesh_range.size(); m++)
         if (st.mesh_range[m].x != st.mesh_range[m].y) {
             s.first_mesh = (int)m;
             s.first_range = st.mesh_range[m];
+            s.first_wide = st.wide.empty() ? -1 : st.mesh_wide[m];
             break;
         }
     ctx->node_num = (int)(st.nodes.size() / 2);
+    ctx->wide_num = (int)(st.wide.size() / 8);
     ctx->tri_num = (int)(st.tri_geom.size() / 3);
     ctx->material_num = (int)st.mats.size();
     ctx->mat_air_n_valid = false;
@@ -504,16 +631,26 @@ bool use_qnodes(const pt_context* ctx) {
     return on && ctx->scene.qnodes != nullptr;
 }
 
+// PT_WIDE=0 keeps pass_kernel_u on the binary nodes even when the scene has wide records.
+bool use_wide(const pt_context* ctx) {
+    static int on = [] {
+        const char* e = getenv("PT_WIDE");
+        return e ? atoi(e) != 0 : true;
+    }();
+    const bool want = ctx->wide_mode >= 0 ? ctx->wide_mode != 0 : on;
+    return want && ctx->scene.wide != nullptr && !use_qnodes(ctx);
+}
+
 // dynamic LDS of pass_kernel_u: every material, then every sphere record (pt_kernels.hip)
 int pass_lds_bytes(const pt_context* ctx) {
     return ctx->material_num * (int)sizeof(DevMaterial) + ctx->scene.sphere_num * 32;
 }
 
 int pass_grid(pt_context* ctx) {
-    const bool leaf1 = ctx->scene.leaf_size == 1, qn = use_qnodes(ctx);
-    int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0][qn ? 1 : 0];
+    const bool leaf1 = ctx->scene.leaf_size == 1, qn = use_qnodes(ctx), wide = use_wide(ctx);
+    int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0][qn ? 1 : (wide ? 2 : 0)];
     if (g == 0) {
-        g = pass_grid_size(leaf1, ctx->instrumented, qn, pass_lds_bytes(ctx));
+        g = pass_grid_size(leaf1, ctx->instrumented, qn, wide, pass_lds_bytes(ctx));
         // PT_GRID_PCT: experiment knob, a percentage of the occupancy-sized grid
         const char* e = getenv("PT_GRID_PCT");
         const int pct = e ? atoi(e) : 100;
@@ -683,7 +820,7 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
         int rc = ev_begin(ctx, 0);
         if (rc != PT_OK) return rc;
-        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, use_qnodes(ctx), first, lg, w8, grid,
+        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, use_qnodes(ctx), use_wide(ctx), first, lg, w8, grid,
                            ctx->instrumented, pass_lds_bytes(ctx), ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         if (lg > 0) {
@@ -794,6 +931,7 @@ extern "C" int pt_scene_upload(pt_context* ctx, int mesh_num, pt_bvh_node_device
         return PT_OK;
     }
     quantise_nodes(*st);
+    build_wide(*st);
     rc = upload_stage(ctx, *st);
     if (timing) std::fprintf(stderr, "[pt] scene upload: translate %.2f ms, quantise+upload -> %.2f ms\n", t_translate, ms());
     if (rc != PT_OK) { ctx->resident.reset(); return rc; }
@@ -806,6 +944,19 @@ extern "C" int pt_scene_info(pt_context* ctx, long long* bytes, int* node_num, i
     if (bytes) *bytes = (long long)ctx->scene_bytes;
     if (node_num) *node_num = ctx->node_num;
     if (triangle_num) *triangle_num = ctx->tri_num;
+    return PT_OK;
+}
+
+extern "C" int pt_set_wide_walk(pt_context* ctx, int mode) {
+    if (!ctx || mode < -1 || mode > 1) { set_error("bad wide walk mode"); return PT_E_ARG; }
+    ctx->wide_mode = mode;
+    return PT_OK;
+}
+
+extern "C" int pt_scene_walk_info(pt_context* ctx, int* wide_records, int* wide_walk) {
+    if (!ctx) return PT_E_ARG;
+    if (wide_records) *wide_records = ctx->wide_num;
+    if (wide_walk) *wide_walk = use_wide(ctx) ? 1 : 0;
     return PT_OK;
 }
 

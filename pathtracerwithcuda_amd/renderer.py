@@ -74,6 +74,16 @@ class Renderer:
         check(self._lib.pt_scene_info(self._ctx, C.byref(b), C.byref(n), C.byref(t)), "pt_scene_info")
         return {"device_bytes": b.value, "nodes": n.value, "triangles": t.value}
 
+    def walk_info(self) -> dict:
+        """Wide BVH records of the resident scene and whether the pass kernel walks them."""
+        n, on = C.c_int(), C.c_int()
+        check(self._lib.pt_scene_walk_info(self._ctx, C.byref(n), C.byref(on)), "pt_scene_walk_info")
+        return {"wide_records": n.value, "wide_walk": bool(on.value)}
+
+    def set_wide_walk(self, on: bool | None) -> None:
+        """True: walk the wide BVH records when the scene has them; False: the binary nodes; None: PT_WIDE."""
+        check(self._lib.pt_set_wide_walk(self._ctx, -1 if on is None else int(bool(on))), "pt_set_wide_walk")
+
     def setup_frame(self, width: int, height: int, image_device_ptr: int | None = None) -> None:
         check(self._lib.pt_frame_setup(self._ctx, width, height, C.c_void_p(image_device_ptr or 0)), "pt_frame_setup")
         self.width, self.height = width, height

@@ -35,12 +35,17 @@ def assert_bitwise(gpu, ref, what=""):
                              f"max |d| {np.nanmax(d):.3g}, mean |d| {np.nanmean(d):.3g}")
 
 
-@pytest.fixture(scope="module", params=["persistent", "wavefront"])
+@pytest.fixture(scope="module", params=["persistent", "persistent_binary", "wavefront"])
 def gpu(require_gpu, request):
-    """Every parity test runs under both kernel schedules (pt_set_schedule): they must agree bitwise."""
+    """Every parity test runs under both kernel schedules (pt_set_schedule), and the persistent one both
+    with its default walk (the wide BVH records where the scene has them, pt_path.h walk_wide) and on the
+    binary nodes only (pt_set_wide_walk): they must all agree bitwise."""
     r = pt.Renderer(0)
-    r.set_schedule(request.param)
-    assert r.schedule() == request.param
+    sched = "wavefront" if request.param == "wavefront" else "persistent"
+    r.set_schedule(sched)
+    assert r.schedule() == sched
+    if request.param == "persistent_binary":
+        r.set_wide_walk(False)
     yield r
     r.close()
 
@@ -135,10 +140,11 @@ def test_instrumented_counts_match_oracle(gpu):
 
 
 @pytest.mark.parametrize("variant", ["ggx_dof", "sss", "glass_knot", "leaf3", "nearest_sky_noaa", "no_gamma",
-                                     "textured", "air_medium"])
+                                     "textured", "air_medium", "axis_aligned_rays"])
 def test_material_and_config_variants(gpu, variant):
     cfg_kw = dict(max_tracer_depth=8)
     cam_kw = dict(BENCH_CAM)
+    W, H = 72, 40
     if variant == "ggx_dof":
         sc = pt.Scene()
         for i, x in enumerate(np.linspace(-2.5, 2.5, 6)):
@@ -177,8 +183,16 @@ def test_material_and_config_variants(gpu, variant):
     elif variant == "air_medium":
         sc = pt.cornell_scene(pt.torus_knot(40, 12), cube_length=32)
         cfg_kw.update(air_absorption_coef=(0.02, 0.03, 0.05), air_reduced_scattering_coef=(0.05, 0.05, 0.05))
+    elif variant == "axis_aligned_rays":
+        # no jitter, yaw 0, pitch 0, odd frame: the centre column's primary rays have d.x == 0 and the
+        # centre row's d.y == 0 exactly, so 1/d is infinite there: those lanes take the binary walk
+        # (walk_wide's exactness argument needs a finite 1/d), the others the wide one
+        sc = pt.cornell_scene(pt.torus_knot(50, 14), cube_length=32)
+        cfg_kw.update(use_anti_alias=0)
+        cam_kw.update(pitch=0.0)
+        W, H = 73, 41
     cfg = pt.configuration(**cfg_kw)
-    cam = pt.camera(72, 40, **cam_kw)
+    cam = pt.camera(W, H, **cam_kw)
     img, img8, ref, ref8, _ = render_both(gpu, sc, cam, cfg, passes=2)
     assert_bitwise(img, ref, f"{variant} float")
     assert_bitwise(img8, ref8, f"{variant} 8-bit")
@@ -345,6 +359,22 @@ def test_schedule_switch_on_one_context(require_gpu):
             img, img8, ref, ref8, _ = render_both(r, sc, cam, cfg, passes=4)
             assert_bitwise(img, ref, f"{sched} {w}x{h} float")
             assert_bitwise(img8, ref8, f"{sched} {w}x{h} 8-bit")
+    finally:
+        r.close()
+
+
+def test_bench_scene_walks_the_wide_records(bench_gpu):
+    """The metric scene gets wide BVH records and the pass kernel walks them by default."""
+    import bench
+    wl = bench.Workload("metric")
+    bench_gpu.upload(wl.scene, wl.cfg)
+    info = bench_gpu.walk_info()
+    assert info["wide_walk"] and info["wide_records"] > 0
+    leaf3 = pt.cornell_scene(pt.torus_knot(30, 10), cube_length=16, leaf_size=3)
+    r = pt.Renderer(0)
+    try:
+        r.upload(leaf3, pt.configuration(bvh_leaf_node_triangle_num=3))
+        assert r.walk_info() == {"wide_records": 0, "wide_walk": False}  # leaf size 1 only
     finally:
         r.close()
 
