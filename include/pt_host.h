@@ -86,6 +86,20 @@ int pt_scene_builder_build_ex(pt_scene_builder* b, int leaf_size, int method, in
 int pt_scene_builder_set_bvh_device(pt_scene_builder* b, int device);
 int pt_scene_builder_view(pt_scene_builder* b, pt_scene_view* out);
 
+/* ---- interactive edits (Core/triangle_mesh.cpp:271-426, Bvh/bvh.cpp:332-356) ------------------
+ * set_transform: triangle_mesh::set_transform_device + update_bvh — the mesh's triangles become
+ *   translate(position) * scale(scale) of its mesh-local triangles and its node boxes are refitted by
+ *   (transform * initial_transform) applied to the corners of its last build (no rebuild).
+ * set_rotate + apply_rotate: the mesh-local triangles are rotated by the change of rotation and the
+ *   mesh's BVH is rebuilt (node arrays may move: fetch the view again).
+ * mesh_local: what pt_mesh_attach (pt_native.h) needs to refit the mesh on a device itself. */
+int pt_scene_builder_set_transform(pt_scene_builder* b, int mesh, pt_float3 position, pt_float3 scale);
+int pt_scene_builder_set_rotate(pt_scene_builder* b, int mesh, pt_float3 rotate);
+int pt_scene_builder_apply_rotate(pt_scene_builder* b, int mesh);
+int pt_scene_builder_mesh_local(pt_scene_builder* b, int mesh, const pt_triangle** local, int* tri_start,
+                                int* tri_count, const pt_bounding_box** init_boxes, int* node_count,
+                                pt_float3* init_position, pt_float3* init_scale);
+
 /* ---- camera (Core/camera.cpp) --------------------------------------------------------------- */
 typedef struct pt_view_camera {
     pt_float3 center;

@@ -44,6 +44,18 @@ int pt_scene_walk_info(pt_context* ctx, int* wide_records, int* wide_walk);
 /* 1: walk the wide records when the scene has them, 0: the binary nodes, -1: PT_WIDE (default 1). */
 int pt_set_wide_walk(pt_context* ctx, int mode);
 
+/* Interactive refit on the device (Core/triangle_mesh.cpp:271-328 + Bvh/bvh.cpp:332-356, which the
+ * reference runs on the host over managed memory). pt_mesh_attach keeps mesh `mesh`'s mesh-local
+ * triangles (tri_count of them, at tri_start in the scene's triangle array), the boxes of its last
+ * build (node_count, the mesh's node count) and that build's transform on the device;
+ * pt_mesh_set_transform then re-transforms the mesh's resident triangles and refits its resident node
+ * boxes in place by one kernel, without re-uploading the scene: the result equals
+ * pt_scene_builder_set_transform's bit for bit. The wide/quantised walks are disabled for a refitted
+ * scene (their records are derived from the pre-refit boxes). */
+int pt_mesh_attach(pt_context* ctx, int mesh, const pt_triangle* local, int tri_start, int tri_count,
+                   const pt_bounding_box* init_boxes, int node_count, pt_float3 init_position, pt_float3 init_scale);
+int pt_mesh_set_transform(pt_context* ctx, int mesh, pt_float3 position, pt_float3 scale);
+
 /* Frame geometry. The image is width*height float3 (12 B/pixel) + uchar3, device resident.
  * image_device: optional caller-owned device buffer (e.g. a torch tensor used for the RCCL
  * reduce); NULL = the context allocates its own. */

@@ -154,6 +154,8 @@ def ref_lib() -> C.CDLL | None:
         h.ptref_png_decode.restype = C.c_int
         h.ptref_png_decode.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                        C.POINTER(C.POINTER(C.c_ubyte))]
+        h.ptref_refit.restype = None
+        h.ptref_refit.argtypes = [C.c_void_p] * 6 + [C.c_int, C.c_void_p, C.c_int] + [C.c_void_p] * 3
         h.ptref_free.restype = None
         h.ptref_free.argtypes = [C.c_void_p]
         _ref = h
@@ -182,6 +184,20 @@ def ref_mesh_load(path: str, position=(0, 0, 0), scale=(1, 1, 1), rotate=(0, 0, 
         for p in (v, n, uv, sh):
             h.ptref_free(p)
     return V, N, U, S, bool(has_uv.value)
+
+
+def ref_refit(init_position, init_scale, position, scale, vertices, normals, boxes):
+    """glm-driven set_transform_device + update_bvh: (world vertices (n,3), normals (n,3), boxes (m,6))."""
+    h = ref_lib()
+    if h is None:
+        raise RuntimeError("oracle/_ref/libptref.so is not built (needs the reference checkout)")
+    f = lambda a: np.ascontiguousarray(a, np.float32)
+    ip, isc, p, sc = f(init_position), f(init_scale), f(position), f(scale)
+    v, n, b = f(vertices).reshape(-1, 3), f(normals).reshape(-1, 3), f(boxes).reshape(-1, 6)
+    vo, no, bo = np.empty_like(v), np.empty_like(n), np.empty_like(b)
+    h.ptref_refit(ip.ctypes.data, isc.ctypes.data, p.ctypes.data, sc.ctypes.data, v.ctypes.data, n.ctypes.data, len(v),
+                  b.ctypes.data, len(b), vo.ctypes.data, no.ctypes.data, bo.ctypes.data)
+    return vo, no, bo
 
 
 def ref_png_decode(path: str) -> np.ndarray:

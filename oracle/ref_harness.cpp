@@ -13,6 +13,7 @@
 //                        followed by Core/triangle_mesh.cpp:625-647 (glm translate * scale,
 //                        normals by its inverse transpose), normalize = Math/cuda_math.hpp:1458
 //                        with the host rsqrtf of :33-36.
+//   ptref_refit       <- Core/triangle_mesh.cpp:271-328 + Bvh/bvh.cpp:332-356 (glm transform, refit)
 //   ptref_png_decode  <- lodepng::decode to RGBA8 (the decoder the reference vendors next to
 //                        Core/cube_map_loader.h:17).
 // Only tests/ link this library; nothing in the product path does.
@@ -128,6 +129,39 @@ int ptref_png_decode(const char* path, int* width, int* height, unsigned char** 
     *rgba = (unsigned char*)malloc(out.size() + 1);
     std::memcpy(*rgba, out.data(), out.size());
     return 0;
+}
+
+// Core/triangle_mesh.cpp:271-328 (set_transform_device) with update_bvh (Bvh/bvh.cpp:332-356), on glm:
+// the transform built as :276-278 (translate then scale), n mesh-local vertices and (normalised) normals
+// -> world vertices and renormalised normals; m boxes (lb.xyz, rt.xyz) of the build made under the
+// initial transform (ipos, iscl; m_mesh_initial_transform = its inverse, :199-204) -> refitted boxes.
+void ptref_refit(const float* ipos, const float* iscl, const float* pos, const float* scl, const float* v,
+                 const float* nrm, int n, const float* boxes, int m, float* v_out, float* n_out, float* boxes_out) {
+    glm::mat4 initial(1.0f);
+    initial = glm::translate(initial, glm::vec3(ipos[0], ipos[1], ipos[2]));
+    initial = glm::scale(initial, glm::vec3(iscl[0], iscl[1], iscl[2]));
+    const glm::mat4 initial_transform_mat = glm::inverse(initial);
+    glm::mat4 transform_mat(1.0f);
+    transform_mat = glm::translate(transform_mat, glm::vec3(pos[0], pos[1], pos[2]));
+    transform_mat = glm::scale(transform_mat, glm::vec3(scl[0], scl[1], scl[2]));
+    const glm::mat4 inverse_transpose_transform_mat = glm::transpose(glm::inverse(transform_mat));
+    for (int i = 0; i < n; i++) {
+        glm::vec4 p(v[3 * i], v[3 * i + 1], v[3 * i + 2], 1.0f);
+        glm::vec4 q(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2], 0.0f);
+        p = transform_mat * p;
+        q = inverse_transpose_transform_mat * q;
+        const F3 nn = ref_normalize({q.x, q.y, q.z});
+        v_out[3 * i] = p.x; v_out[3 * i + 1] = p.y; v_out[3 * i + 2] = p.z;
+        n_out[3 * i] = nn.x; n_out[3 * i + 1] = nn.y; n_out[3 * i + 2] = nn.z;
+    }
+    for (int j = 0; j < m; j++) {
+        glm::vec4 lb(boxes[6 * j], boxes[6 * j + 1], boxes[6 * j + 2], 1.0f);
+        glm::vec4 rt(boxes[6 * j + 3], boxes[6 * j + 4], boxes[6 * j + 5], 1.0f);
+        lb = transform_mat * initial_transform_mat * lb;
+        rt = transform_mat * initial_transform_mat * rt;
+        boxes_out[6 * j] = lb.x; boxes_out[6 * j + 1] = lb.y; boxes_out[6 * j + 2] = lb.z;
+        boxes_out[6 * j + 3] = rt.x; boxes_out[6 * j + 4] = rt.y; boxes_out[6 * j + 5] = rt.z;
+    }
 }
 
 void ptref_free(void* p) { free(p); }

@@ -191,6 +191,9 @@ _PROTOS = {
     "pt_scene_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong), c_int_p, c_int_p]),
     "pt_scene_walk_info": (C.c_int, [C.c_void_p, c_int_p, c_int_p]),
     "pt_set_wide_walk": (C.c_int, [C.c_void_p, C.c_int]),
+    "pt_mesh_attach": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Triangle), C.c_int, C.c_int, C.POINTER(BoundingBox),
+                                 C.c_int, Float3, Float3]),
+    "pt_mesh_set_transform": (C.c_int, [C.c_void_p, C.c_int, Float3, Float3]),
     "pt_frame_setup": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "pt_set_tiling": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
     "pt_render_passes": (C.c_int, [C.c_void_p, C.POINTER(RenderCamera), C.POINTER(Configuration), C.c_int, C.c_int,
@@ -226,6 +229,12 @@ _PROTOS = {
     "pt_scene_builder_add_texture": (C.c_int, [C.c_void_p, C.c_int, C.c_int, c_ubyte_p]),
     "pt_scene_builder_build": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "pt_scene_builder_view": (C.c_int, [C.c_void_p, C.POINTER(SceneView)]),
+    "pt_scene_builder_set_transform": (C.c_int, [C.c_void_p, C.c_int, Float3, Float3]),
+    "pt_scene_builder_set_rotate": (C.c_int, [C.c_void_p, C.c_int, Float3]),
+    "pt_scene_builder_apply_rotate": (C.c_int, [C.c_void_p, C.c_int]),
+    "pt_scene_builder_mesh_local": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.POINTER(Triangle)), c_int_p, c_int_p,
+                                              C.POINTER(C.POINTER(BoundingBox)), c_int_p, C.POINTER(Float3),
+                                              C.POINTER(Float3)]),
     "pt_view_camera_default": (None, [C.POINTER(ViewCamera)]),
     "pt_view_camera_set_resolution": (None, [C.POINTER(ViewCamera), C.c_float, C.c_float]),
     "pt_view_camera_set_fov": (None, [C.POINTER(ViewCamera), C.c_float]),

@@ -11,6 +11,7 @@
 #include "pt_bvh_internal.h"
 #include "../../include/pt_bvh.h"
 #include "../../include/pt_native.h"
+#include "pt_glm.h"
 
 namespace {
 
@@ -435,6 +436,16 @@ struct pt_scene_builder {
     std::vector<pt_triangle> triangles;
     std::vector<int> tri_material;
     std::vector<int> mesh_start, mesh_count;
+    // the interactive-edit state of Core/triangle_mesh.h: mesh-local triangles (m_triangles: loaded and
+    // rotated, before translate * scale), position / scale / rotate and the rotation already applied,
+    // the inverse of the transform the BVH was built under (m_mesh_initial_transform) and the boxes of
+    // that build (m_mesh_bvh_initial_device)
+    std::vector<pt_triangle> local;
+    std::vector<pt_float3> mesh_pos, mesh_scl, mesh_rot, mesh_rot_applied;
+    std::vector<ptglm::M4> init_inv;
+    std::vector<pt_float3> init_pos, init_scl;  // the transform init_inv inverts
+    std::vector<std::vector<pt_bounding_box>> init_boxes;
+    int build_leaf = 1, build_method = 2, build_bucket = 12;
     std::vector<std::vector<unsigned char>> textures;
     std::vector<int> tex_w, tex_h;
     std::vector<unsigned char> cube;
@@ -478,34 +489,10 @@ extern "C" int pt_scene_builder_add_sphere(pt_scene_builder* b, pt_float3 center
 }
 
 namespace {
-// ---- glm 0.9.9 float matrices as the mesh loader uses them (lib/glm) ----------------------------
-// Column-major like glm: c[col][row]. Every expression keeps glm's evaluation order so that,
-// with contraction off, the transformed vertices and normals round as the reference's do.
-struct M4 {
-    float c[4][4];
-};
-M4 identity4() {
-    M4 m;
-    for (int i = 0; i < 4; i++)
-        for (int j = 0; j < 4; j++) m.c[i][j] = i == j ? 1.0f : 0.0f;
-    return m;
-}
-struct V4 {
-    float x, y, z, w;
-};
-inline V4 add4(V4 a, V4 b) { return {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
-inline V4 mul4(V4 a, float s) { return {a.x * s, a.y * s, a.z * s, a.w * s}; }
-inline V4 mul4v(V4 a, V4 b) { return {a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w}; }
-inline V4 sub4(V4 a, V4 b) { return {a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w}; }
-inline V4 col(const M4& m, int i) { return {m.c[i][0], m.c[i][1], m.c[i][2], m.c[i][3]}; }
-inline void set_col(M4& m, int i, V4 v) { m.c[i][0] = v.x; m.c[i][1] = v.y; m.c[i][2] = v.z; m.c[i][3] = v.w; }
+using namespace ptglm;
 
-// operator*(mat4, vec4) (glm/detail/type_mat4x4.inl:505-524): (m0*x + m1*y) + (m2*z + m3*w)
-V4 mat_vec(const M4& m, V4 v) {
-    return add4(add4(mul4(col(m, 0), v.x), mul4(col(m, 1), v.y)), add4(mul4(col(m, 2), v.z), mul4(col(m, 3), v.w)));
-}
-
-// glm::rotate (glm/gtc/matrix_transform.inl:18-47) about a unit coordinate axis
+// glm::rotate (glm/gtc/matrix_transform.inl:18-47) about a unit coordinate axis (host libm cos/sin, as
+// the reference's host code)
 M4 rotate4(const M4& m, float angle, int axis_index) {
     const float c = std::cos(angle), s = std::sin(angle);
     float axis[3] = {0.0f, 0.0f, 0.0f};
@@ -528,54 +515,10 @@ M4 rotate4(const M4& m, float angle, int axis_index) {
     return r;
 }
 
-// glm::inverse, generic 4x4 path (glm/detail/func_matrix.inl:296-355)
-M4 inverse4(const M4& M) {
-    auto m = [&](int a, int b) { return M.c[a][b]; };
-    float c00 = m(2, 2) * m(3, 3) - m(3, 2) * m(2, 3), c02 = m(1, 2) * m(3, 3) - m(3, 2) * m(1, 3);
-    float c03 = m(1, 2) * m(2, 3) - m(2, 2) * m(1, 3);
-    float c04 = m(2, 1) * m(3, 3) - m(3, 1) * m(2, 3), c06 = m(1, 1) * m(3, 3) - m(3, 1) * m(1, 3);
-    float c07 = m(1, 1) * m(2, 3) - m(2, 1) * m(1, 3);
-    float c08 = m(2, 1) * m(3, 2) - m(3, 1) * m(2, 2), c10 = m(1, 1) * m(3, 2) - m(3, 1) * m(1, 2);
-    float c11 = m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2);
-    float c12 = m(2, 0) * m(3, 3) - m(3, 0) * m(2, 3), c14 = m(1, 0) * m(3, 3) - m(3, 0) * m(1, 3);
-    float c15 = m(1, 0) * m(2, 3) - m(2, 0) * m(1, 3);
-    float c16 = m(2, 0) * m(3, 2) - m(3, 0) * m(2, 2), c18 = m(1, 0) * m(3, 2) - m(3, 0) * m(1, 2);
-    float c19 = m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2);
-    float c20 = m(2, 0) * m(3, 1) - m(3, 0) * m(2, 1), c22 = m(1, 0) * m(3, 1) - m(3, 0) * m(1, 1);
-    float c23 = m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1);
-    V4 f0{c00, c00, c02, c03}, f1{c04, c04, c06, c07}, f2{c08, c08, c10, c11};
-    V4 f3{c12, c12, c14, c15}, f4{c16, c16, c18, c19}, f5{c20, c20, c22, c23};
-    V4 v0{m(1, 0), m(0, 0), m(0, 0), m(0, 0)}, v1{m(1, 1), m(0, 1), m(0, 1), m(0, 1)};
-    V4 v2{m(1, 2), m(0, 2), m(0, 2), m(0, 2)}, v3{m(1, 3), m(0, 3), m(0, 3), m(0, 3)};
-    V4 i0 = add4(sub4(mul4v(v1, f0), mul4v(v2, f1)), mul4v(v3, f2));
-    V4 i1 = add4(sub4(mul4v(v0, f0), mul4v(v2, f3)), mul4v(v3, f4));
-    V4 i2 = add4(sub4(mul4v(v0, f1), mul4v(v1, f3)), mul4v(v3, f5));
-    V4 i3 = add4(sub4(mul4v(v0, f2), mul4v(v1, f4)), mul4v(v2, f5));
-    const V4 sa{+1, -1, +1, -1}, sb{-1, +1, -1, +1};
-    M4 inv;
-    set_col(inv, 0, mul4v(i0, sa));
-    set_col(inv, 1, mul4v(i1, sb));
-    set_col(inv, 2, mul4v(i2, sa));
-    set_col(inv, 3, mul4v(i3, sb));
-    V4 row0{inv.c[0][0], inv.c[1][0], inv.c[2][0], inv.c[3][0]};
-    V4 dot0 = mul4v(col(M, 0), row0);
-    float dot1 = (dot0.x + dot0.y) + (dot0.z + dot0.w);
-    float one_over_det = 1.0f / dot1;
-    for (int i = 0; i < 4; i++) set_col(inv, i, mul4(col(inv, i), one_over_det));
-    return inv;
-}
-
-M4 transpose4(const M4& m) {
-    M4 t;
-    for (int i = 0; i < 4; i++)
-        for (int j = 0; j < 4; j++) t.c[i][j] = m.c[j][i];
-    return t;
-}
-
-// normalize with the host rsqrtf = 1 / sqrtf (Math/cuda_math.hpp:33-36, :1458-1462)
 inline pt_float3 normalize_host(float x, float y, float z) {
-    const float inv = 1.0f / std::sqrt(x * x + y * y + z * z);
-    return {x * inv, y * inv, z * inv};
+    float o[3];
+    normalize3(x, y, z, o);
+    return {o[0], o[1], o[2]};
 }
 }  // namespace
 
@@ -600,9 +543,18 @@ extern "C" int pt_scene_builder_add_mesh(pt_scene_builder* b, int tri_num, const
     const M4 Tn = transpose4(inverse4(T));
     b->mesh_start.push_back((int)b->triangles.size());
     b->mesh_count.push_back(tri_num);
+    b->mesh_pos.push_back(pos);
+    b->mesh_scl.push_back(scl);
+    b->mesh_rot.push_back(rot);
+    b->mesh_rot_applied.push_back(rot);
+    b->init_inv.push_back(inverse4(T));
+    b->init_pos.push_back(pos);
+    b->init_scl.push_back(scl);
+    b->init_boxes.emplace_back();
     for (int t = 0; t < tri_num; t++) {
-        pt_triangle tr;
+        pt_triangle tr, lt;
         std::memset(&tr, 0, sizeof(tr));
+        std::memset(&lt, 0, sizeof(lt));
         pt_float3* vo[3] = {&tr.vertex0, &tr.vertex1, &tr.vertex2};
         pt_float3* no[3] = {&tr.normal0, &tr.normal1, &tr.normal2};
         pt_float2* uo[3] = {&tr.uv0, &tr.uv1, &tr.uv2};
@@ -616,10 +568,13 @@ extern "C" int pt_scene_builder_add_mesh(pt_scene_builder* b, int tri_num, const
             const V4 wn = mat_vec(Tn, V4{n1.x, n1.y, n1.z, 0.0f});
             *vo[k] = {wv.x, wv.y, wv.z};
             *no[k] = normalize_host(wn.x, wn.y, wn.z);
+            (&lt.vertex0)[k] = {rv.x, rv.y, rv.z};
+            (&lt.normal0)[k] = n1;
             if (uv) *uo[k] = {uv[(size_t)t * 6 + k * 2], uv[(size_t)t * 6 + k * 2 + 1]};
             else *uo[k] = {0.0f, 0.0f};
         }
         b->triangles.push_back(tr);
+        b->local.push_back(lt);
         b->tri_material.push_back(tri_material[t]);
     }
     b->built = false;
@@ -654,6 +609,32 @@ extern "C" int pt_scene_builder_set_bvh_device(pt_scene_builder* b, int device) 
     return 0;
 }
 
+namespace {
+// One mesh's BVH with the builder's configured method (MortonCodeCUDA on the GPU when present).
+int build_mesh_bvh(pt_scene_builder* b, size_t m, pt_bvh_node_device** nodes, int* nn, int** leaf, int* ln) {
+    // MortonCodeCUDA runs on the GPU (pt_bvh.hip); its node array equals the host builder's bit for bit
+    // (tests/test_bvh_device.py), which therefore serves machines without a HIP device
+    const bool on_device = b->build_method == PT_BVH_MORTON_CODE_CUDA &&
+                           (b->bvh_device >= 0 || (b->bvh_device == -2 && pt_device_count() > 0));
+    return on_device ? pt_bvh_build_device(b->triangles.data() + b->mesh_start[m], b->mesh_count[m], b->mesh_start[m],
+                                           b->build_leaf, nodes, nn, leaf, ln)
+                     : pt_bvh_build_ex(b->triangles.data() + b->mesh_start[m], b->mesh_count[m], b->mesh_start[m],
+                                       b->build_leaf, b->build_method, b->build_bucket, nodes, nn, leaf, ln);
+}
+
+// The boxes of a fresh build are the mesh's initial boxes, under its current transform
+// (Core/triangle_mesh.cpp:498-540 keeps the first device copy as m_mesh_bvh_initial_device).
+void snapshot_initial(pt_scene_builder* b, size_t m) {
+    const pt_bvh_node_device* nodes = b->bvh_nodes[m];
+    b->init_boxes[m].resize((size_t)b->node_num[m]);
+    for (int i = 0; i < b->node_num[m]; i++) b->init_boxes[m][i] = nodes[i].box;
+    const pt_float3 p = b->mesh_pos[m], s = b->mesh_scl[m];
+    b->init_inv[m] = inverse4(translate_scale(p.x, p.y, p.z, s.x, s.y, s.z));
+    b->init_pos[m] = p;
+    b->init_scl[m] = s;
+}
+}  // namespace
+
 extern "C" int pt_scene_builder_build_ex(pt_scene_builder* b, int leaf_size, int method, int bucket_num) {
     if (!b) return -1;
     b->release_bvh();
@@ -662,21 +643,18 @@ extern "C" int pt_scene_builder_build_ex(pt_scene_builder* b, int leaf_size, int
         if (m < 0 || m >= (int)b->materials.size()) return -3;
         b->triangles[t].mat = b->materials.data() + m;
     }
+    b->build_leaf = leaf_size;
+    b->build_method = method;
+    b->build_bucket = bucket_num;
     for (size_t m = 0; m < b->mesh_start.size(); m++) {
         pt_bvh_node_device* nodes = nullptr;
         int nn = 0, *leaf = nullptr, ln = 0;
-        // MortonCodeCUDA runs on the GPU (pt_bvh.hip); its node array equals the host builder's bit for bit
-        // (tests/test_bvh_device.py), which therefore serves machines without a HIP device
-        const bool on_device = method == PT_BVH_MORTON_CODE_CUDA &&
-                               (b->bvh_device >= 0 || (b->bvh_device == -2 && pt_device_count() > 0));
-        int rc = on_device ? pt_bvh_build_device(b->triangles.data() + b->mesh_start[m], b->mesh_count[m],
-                                                 b->mesh_start[m], leaf_size, &nodes, &nn, &leaf, &ln)
-                           : pt_bvh_build_ex(b->triangles.data() + b->mesh_start[m], b->mesh_count[m], b->mesh_start[m],
-                                             leaf_size, method, bucket_num, &nodes, &nn, &leaf, &ln);
+        int rc = build_mesh_bvh(b, m, &nodes, &nn, &leaf, &ln);
         if (rc != 0) return rc;
         b->bvh_nodes.push_back(nodes);
         b->bvh_leaf.push_back(leaf);
         b->node_num.push_back(nn);
+        snapshot_initial(b, m);
     }
     b->tex_wrappers.clear();
     for (size_t i = 0; i < b->textures.size(); i++)
@@ -687,6 +665,108 @@ extern "C" int pt_scene_builder_build_ex(pt_scene_builder* b, int leaf_size, int
         b->cube_map = {base, base + face, base + 2 * face, base + 3 * face, base + 4 * face, base + 5 * face, b->cube_len};
     }
     b->built = true;
+    return 0;
+}
+
+// triangle_mesh::set_transform_device (Core/triangle_mesh.cpp:271-328) with bvh_update_function = update_bvh
+// (Bvh/bvh.cpp:332-356): the mesh's triangles become translate(position) * scale(scale) applied to its
+// mesh-local triangles (normals by the inverse transpose, renormalised); every node box becomes
+// (transform * initial_transform) applied to its two corners in the initial build, centroid = their mean.
+extern "C" int pt_scene_builder_set_transform(pt_scene_builder* b, int mesh, pt_float3 position, pt_float3 scale) {
+    if (!b || !b->built || mesh < 0 || mesh >= (int)b->mesh_start.size()) return -1;
+    const M4 T = translate_scale(position.x, position.y, position.z, scale.x, scale.y, scale.z);
+    const M4 Tn = transpose4(inverse4(T));
+    b->mesh_pos[mesh] = position;
+    b->mesh_scl[mesh] = scale;
+    for (int t = b->mesh_start[mesh]; t < b->mesh_start[mesh] + b->mesh_count[mesh]; t++) {
+        const pt_triangle& lt = b->local[t];
+        pt_triangle& tr = b->triangles[t];
+        for (int k = 0; k < 3; k++) {
+            const pt_float3 v = (&lt.vertex0)[k], n = (&lt.normal0)[k];
+            const V4 wv = mat_vec(T, V4{v.x, v.y, v.z, 1.0f});
+            const V4 wn = mat_vec(Tn, V4{n.x, n.y, n.z, 0.0f});
+            (&tr.vertex0)[k] = {wv.x, wv.y, wv.z};
+            (&tr.normal0)[k] = normalize_host(wn.x, wn.y, wn.z);
+        }
+    }
+    const M4 C = mat_mul(T, b->init_inv[mesh]);  // transform_mat * initial_transform_mat (bvh.cpp:348-349)
+    pt_bvh_node_device* nodes = b->bvh_nodes[mesh];
+    for (int i = 0; i < b->node_num[mesh]; i++) {
+        const pt_bounding_box& ib = b->init_boxes[mesh][i];
+        const V4 lb = mat_vec(C, V4{ib.left_bottom.x, ib.left_bottom.y, ib.left_bottom.z, 1.0f});
+        const V4 rt = mat_vec(C, V4{ib.right_top.x, ib.right_top.y, ib.right_top.z, 1.0f});
+        pt_bounding_box& bx = nodes[i].box;
+        bx.left_bottom = {lb.x, lb.y, lb.z};
+        bx.right_top = {rt.x, rt.y, rt.z};
+        bx.centroid = {0.5f * (lb.x + rt.x), 0.5f * (lb.y + rt.y), 0.5f * (lb.z + rt.z)};
+    }
+    return 0;
+}
+
+// triangle_mesh::set_rotate (:330-333) + apply_rotate (:335-426): the mesh-local triangles are rotated
+// by the change of rotation (Z, then Y, then X, in degrees), the mesh is re-transformed, the initial
+// transform becomes the inverse of the current one and the mesh's BVH is rebuilt.
+extern "C" int pt_scene_builder_set_rotate(pt_scene_builder* b, int mesh, pt_float3 rotate) {
+    if (!b || mesh < 0 || mesh >= (int)b->mesh_start.size()) return -1;
+    b->mesh_rot[mesh] = rotate;
+    return 0;
+}
+
+extern "C" int pt_scene_builder_apply_rotate(pt_scene_builder* b, int mesh) {
+    if (!b || !b->built || mesh < 0 || mesh >= (int)b->mesh_start.size()) return -1;
+    const float deg = 0.01745329251994329576923690768489f;  // glm::radians
+    const pt_float3 r = b->mesh_rot[mesh], a = b->mesh_rot_applied[mesh];
+    M4 R = identity4();
+    R = rotate4(R, (r.z - a.z) * deg, 2);
+    R = rotate4(R, (r.y - a.y) * deg, 1);
+    R = rotate4(R, (r.x - a.x) * deg, 0);
+    const M4 Rn = transpose4(inverse4(R));
+    const pt_float3 p = b->mesh_pos[mesh], s = b->mesh_scl[mesh];
+    const M4 T = translate_scale(p.x, p.y, p.z, s.x, s.y, s.z);
+    const M4 Tn = transpose4(inverse4(T));
+    for (int t = b->mesh_start[mesh]; t < b->mesh_start[mesh] + b->mesh_count[mesh]; t++) {
+        pt_triangle& lt = b->local[t];
+        pt_triangle& tr = b->triangles[t];
+        for (int k = 0; k < 3; k++) {
+            const pt_float3 v = (&lt.vertex0)[k], n = (&lt.normal0)[k];
+            const V4 rv = mat_vec(R, V4{v.x, v.y, v.z, 1.0f});
+            const V4 rn = mat_vec(Rn, V4{n.x, n.y, n.z, 0.0f});
+            const pt_float3 n1 = normalize_host(rn.x, rn.y, rn.z);
+            (&lt.vertex0)[k] = {rv.x, rv.y, rv.z};
+            (&lt.normal0)[k] = n1;
+            const V4 wv = mat_vec(T, V4{rv.x, rv.y, rv.z, 1.0f});
+            const V4 wn = mat_vec(Tn, V4{n1.x, n1.y, n1.z, 0.0f});
+            (&tr.vertex0)[k] = {wv.x, wv.y, wv.z};
+            (&tr.normal0)[k] = normalize_host(wn.x, wn.y, wn.z);
+        }
+    }
+    pt_bvh_node_device* nodes = nullptr;
+    int nn = 0, *leaf = nullptr, ln = 0;
+    int rc = build_mesh_bvh(b, (size_t)mesh, &nodes, &nn, &leaf, &ln);
+    if (rc != 0) return rc;
+    pt_bvh_free(b->bvh_nodes[mesh], b->bvh_leaf[mesh]);
+    b->bvh_nodes[mesh] = nodes;
+    b->bvh_leaf[mesh] = leaf;
+    b->node_num[mesh] = nn;
+    snapshot_initial(b, (size_t)mesh);
+    b->mesh_rot_applied[mesh] = b->mesh_rot[mesh];
+    return 0;
+}
+
+// What a device context needs to refit one mesh itself (pt_mesh_attach): its mesh-local triangles,
+// where they start in the triangle array, the boxes of its last build and the transform (position,
+// scale) that build was made under.
+extern "C" int pt_scene_builder_mesh_local(pt_scene_builder* b, int mesh, const pt_triangle** local, int* tri_start,
+                                           int* tri_count, const pt_bounding_box** init_boxes, int* node_count,
+                                           pt_float3* init_position, pt_float3* init_scale) {
+    if (!b || !b->built || mesh < 0 || mesh >= (int)b->mesh_start.size()) return -1;
+    if (local) *local = b->local.data() + b->mesh_start[mesh];
+    if (tri_start) *tri_start = b->mesh_start[mesh];
+    if (tri_count) *tri_count = b->mesh_count[mesh];
+    if (init_boxes) *init_boxes = b->init_boxes[mesh].data();
+    if (node_count) *node_count = (int)b->init_boxes[mesh].size();
+    if (init_position) *init_position = b->init_pos[mesh];
+    if (init_scale) *init_scale = b->init_scl[mesh];
     return 0;
 }
 

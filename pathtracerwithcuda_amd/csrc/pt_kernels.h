@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "pt_glm.h"
 #include "pt_path.h"
 #include "pt_work.h"
 
@@ -27,6 +28,9 @@ hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256
 int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int lds_bytes);  // lds_bytes: pass_kernel_u's dynamic LDS
 int env_int(const char* name, int dflt, int lo, int hi);  // clamped integer from the environment
 hipError_t launch_material_consts(DevMaterial* mats, int n, float air_n, hipStream_t stream);
+hipError_t launch_mesh_refit(const float4* local, int tri_start, int tri_count, const float4* init_nodes, int node_first,
+                             int node_count, const ptglm::M4& T, const ptglm::M4& Tn, const ptglm::M4& C,
+                             float4* tri_geom, float4* tri_shade, float4* nodes, hipStream_t stream);
 hipError_t launch_math_eval(int which, const float* x, int n, float* o0, float* o1, hipStream_t stream);
 hipError_t shrink(int* data, int n, int* scratch, int* tile_counts, int* total_dev, int* total_host,
                   hipStream_t stream);

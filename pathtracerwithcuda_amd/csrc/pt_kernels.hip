@@ -531,6 +531,61 @@ hipError_t launch_material_consts(DevMaterial* mats, int n, float air_n, hipStre
     return hipGetLastError();
 }
 
+// Interactive refit of one mesh (pt_mesh_set_transform; Core/triangle_mesh.cpp:271-328, Bvh/bvh.cpp:
+// 332-356): thread i re-transforms mesh-local triangle i into the resident triangle records (edges of
+// triangle::intersect as translate_scene computes them, normals into tri_shade) and refits node i's box
+// from its initial corners. pt_glm.h keeps glm's operation order, so the result equals the host
+// builder's pt_scene_builder_set_transform bit for bit.
+__global__ __launch_bounds__(PT_BLOCK) void mesh_refit_kernel(const float4* __restrict__ local, int tri_start,
+                                                              int tri_count, const float4* __restrict__ init_nodes,
+                                                              int node_first, int node_count, ptglm::M4 T, ptglm::M4 Tn,
+                                                              ptglm::M4 C, float4* tri_geom, float4* tri_shade,
+                                                              float4* nodes) {
+    using namespace ptglm;
+    const int i = blockIdx.x * PT_BLOCK + threadIdx.x;
+    if (i < tri_count) {
+        float v[3][3], n[3][3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const float4 lv = local[6 * (size_t)i + k], ln = local[6 * (size_t)i + 3 + k];
+            const V4 wv = mat_vec(T, V4{lv.x, lv.y, lv.z, 1.0f});
+            const V4 wn = mat_vec(Tn, V4{ln.x, ln.y, ln.z, 0.0f});
+            v[k][0] = wv.x; v[k][1] = wv.y; v[k][2] = wv.z;
+            normalize3(wn.x, wn.y, wn.z, n[k]);
+        }
+        const size_t t = (size_t)tri_start + i;
+        tri_geom[3 * t] = make_float4(v[0][0], v[0][1], v[0][2], 0.0f);
+        tri_geom[3 * t + 1] = make_float4(v[1][0] - v[0][0], v[1][1] - v[0][1], v[1][2] - v[0][2], 0.0f);
+        tri_geom[3 * t + 2] = make_float4(v[2][0] - v[0][0], v[2][1] - v[0][1], v[2][2] - v[0][2], 0.0f);
+        float4 s2 = tri_shade[4 * t + 2];
+        tri_shade[4 * t] = make_float4(n[0][0], n[0][1], n[0][2], n[1][0]);
+        tri_shade[4 * t + 1] = make_float4(n[1][1], n[1][2], n[2][0], n[2][1]);
+        s2.x = n[2][2];
+        tri_shade[4 * t + 2] = s2;
+    }
+    if (i < node_count) {
+        const float4 lb = init_nodes[2 * (size_t)i], rt = init_nodes[2 * (size_t)i + 1];
+        const V4 a = mat_vec(C, V4{lb.x, lb.y, lb.z, 1.0f});
+        const V4 b = mat_vec(C, V4{rt.x, rt.y, rt.z, 1.0f});
+        const size_t k = 2 * ((size_t)node_first + i);
+        float4 na = nodes[k], nb = nodes[k + 1];
+        na.x = a.x; na.y = a.y; na.z = a.z;
+        nb.x = b.x; nb.y = b.y; nb.z = b.z;
+        nodes[k] = na;
+        nodes[k + 1] = nb;
+    }
+}
+
+hipError_t launch_mesh_refit(const float4* local, int tri_start, int tri_count, const float4* init_nodes, int node_first,
+                             int node_count, const ptglm::M4& T, const ptglm::M4& Tn, const ptglm::M4& C,
+                             float4* tri_geom, float4* tri_shade, float4* nodes, hipStream_t stream) {
+    const int n = tri_count > node_count ? tri_count : node_count;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mesh_refit_kernel, dim3((n + PT_BLOCK - 1) / PT_BLOCK), dim3(PT_BLOCK), 0, stream, local,
+                       tri_start, tri_count, init_nodes, node_first, node_count, T, Tn, C, tri_geom, tri_shade, nodes);
+    return hipGetLastError();
+}
+
 // Diagnostic: the device transcendentals on an array (bitwise check against the oracle's).
 __global__ __launch_bounds__(PT_BLOCK) void math_eval_kernel(int which, const float* x, int n, float* o0, float* o1) {
     int i = blockIdx.x * PT_BLOCK + threadIdx.x;

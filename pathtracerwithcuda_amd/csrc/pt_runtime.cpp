@@ -26,6 +26,10 @@
 using namespace pt;
 
 namespace {
+void free_refit(pt_context* ctx);
+}
+
+namespace {
 
 thread_local std::string g_last_error;
 
@@ -486,6 +490,16 @@ struct pt_context {
     // host copy of the resident scene's translation: an upload of identical content (the reference
     // caller re-sends the scene on every pass_counter == 1, i.e. after every camera move) keeps it
     std::unique_ptr<SceneStage> resident;
+    std::vector<int2> mesh_range;  // node range per mesh of the resident scene
+    // pt_mesh_attach: per mesh, device copies of its mesh-local triangles (v0..v2, n0..n2 as float4) and
+    // initial node corners, and the inverse of the transform of those boxes
+    struct MeshRefit {
+        void* mem = nullptr;
+        int tri_start = 0, tri_count = 0, node_count = 0;
+        ptglm::M4 init_inv{};
+    };
+    std::unordered_map<int, MeshRefit> refit;
+    bool refitted = false;  // a mesh was refitted: the wide / quantised records are stale
 };
 
 namespace {
@@ -495,7 +509,15 @@ int ensure_device(pt_context* ctx) {
     return PT_OK;
 }
 
+void free_refit(pt_context* ctx) {
+    for (auto& kv : ctx->refit)
+        if (kv.second.mem) (void)hipFree(kv.second.mem);
+    ctx->refit.clear();
+    ctx->refitted = false;
+}
+
 void free_scene(pt_context* ctx) {
+    free_refit(ctx);
     if (ctx->scene_mem) (void)hipFree(ctx->scene_mem);
     ctx->scene_mem = nullptr;
     ctx->scene_bytes = 0;
@@ -570,6 +592,7 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
         }
     ctx->node_num = (int)(st.nodes.size() / 2);
     ctx->wide_num = (int)(st.wide.size() / 8);
+    ctx->mesh_range = st.mesh_range;
     ctx->tri_num = (int)(st.tri_geom.size() / 3);
     ctx->material_num = (int)st.mats.size();
     ctx->mat_air_n_valid = false;
@@ -628,7 +651,7 @@ bool use_qnodes(const pt_context* ctx) {
         const char* e = getenv("PT_QNODES");
         return e && atoi(e) != 0;
     }();
-    return on && ctx->scene.qnodes != nullptr;
+    return on && ctx->scene.qnodes != nullptr && !ctx->refitted;
 }
 
 // PT_WIDE=0 keeps pass_kernel_u on the binary nodes even when the scene has wide records.
@@ -638,7 +661,7 @@ bool use_wide(const pt_context* ctx) {
         return e ? atoi(e) != 0 : true;
     }();
     const bool want = ctx->wide_mode >= 0 ? ctx->wide_mode != 0 : on;
-    return want && ctx->scene.wide != nullptr && !use_qnodes(ctx);
+    return want && ctx->scene.wide != nullptr && !ctx->refitted && !use_qnodes(ctx);
 }
 
 // dynamic LDS of pass_kernel_u: every material, then every sphere record (pt_kernels.hip)
@@ -950,6 +973,69 @@ extern "C" int pt_scene_info(pt_context* ctx, long long* bytes, int* node_num, i
 extern "C" int pt_set_wide_walk(pt_context* ctx, int mode) {
     if (!ctx || mode < -1 || mode > 1) { set_error("bad wide walk mode"); return PT_E_ARG; }
     ctx->wide_mode = mode;
+    return PT_OK;
+}
+
+extern "C" int pt_mesh_attach(pt_context* ctx, int mesh, const pt_triangle* local, int tri_start, int tri_count,
+                              const pt_bounding_box* init_boxes, int node_count, pt_float3 init_position,
+                              pt_float3 init_scale) {
+    if (!ctx || !ctx->has_scene) { set_error("no scene uploaded"); return PT_E_STATE; }
+    if (mesh < 0 || mesh >= (int)ctx->mesh_range.size() || !local || !init_boxes || tri_count <= 0 || tri_start < 0 ||
+        tri_start + tri_count > ctx->tri_num) {
+        set_error("pt_mesh_attach: bad mesh / triangle range");
+        return PT_E_ARG;
+    }
+    const int2 r = ctx->mesh_range[mesh];
+    if (node_count != r.y - r.x) { set_error("pt_mesh_attach: %d boxes for a mesh of %d nodes", node_count, r.y - r.x); return PT_E_ARG; }
+    int rc = ensure_device(ctx);
+    if (rc != PT_OK) return rc;
+    std::vector<float4> h((size_t)tri_count * 6 + (size_t)node_count * 2);
+    for (int i = 0; i < tri_count; i++) {
+        const pt_triangle& t = local[i];
+        const pt_float3 c[6] = {t.vertex0, t.vertex1, t.vertex2, t.normal0, t.normal1, t.normal2};
+        for (int k = 0; k < 6; k++) h[(size_t)i * 6 + k] = mkf4(c[k].x, c[k].y, c[k].z, 0.0f);
+    }
+    float4* hb = h.data() + (size_t)tri_count * 6;
+    for (int i = 0; i < node_count; i++) {
+        const pt_bounding_box& b = init_boxes[i];
+        hb[2 * i] = mkf4(b.left_bottom.x, b.left_bottom.y, b.left_bottom.z, 0.0f);
+        hb[2 * i + 1] = mkf4(b.right_top.x, b.right_top.y, b.right_top.z, 0.0f);
+    }
+    pt_context::MeshRefit m;
+    PT_HIP(hipMalloc(&m.mem, h.size() * sizeof(float4)));
+    hipError_t e = hipMemcpyAsync(m.mem, h.data(), h.size() * sizeof(float4), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) { (void)hipFree(m.mem); PT_HIP(e); }
+    m.tri_start = tri_start;
+    m.tri_count = tri_count;
+    m.node_count = node_count;
+    m.init_inv = ptglm::inverse4(ptglm::translate_scale(init_position.x, init_position.y, init_position.z, init_scale.x,
+                                                        init_scale.y, init_scale.z));
+    auto it = ctx->refit.find(mesh);
+    if (it != ctx->refit.end() && it->second.mem) (void)hipFree(it->second.mem);
+    ctx->refit[mesh] = m;
+    return PT_OK;
+}
+
+extern "C" int pt_mesh_set_transform(pt_context* ctx, int mesh, pt_float3 position, pt_float3 scale) {
+    if (!ctx || !ctx->has_scene) { set_error("no scene uploaded"); return PT_E_STATE; }
+    auto it = ctx->refit.find(mesh);
+    if (it == ctx->refit.end()) { set_error("pt_mesh_set_transform: mesh %d not attached (pt_mesh_attach)", mesh); return PT_E_STATE; }
+    int rc = ensure_device(ctx);
+    if (rc != PT_OK) return rc;
+    const pt_context::MeshRefit& m = it->second;
+    // Core/triangle_mesh.cpp:276-278 (translate * scale), :307 (inverse transpose), Bvh/bvh.cpp:348-349
+    const ptglm::M4 T = ptglm::translate_scale(position.x, position.y, position.z, scale.x, scale.y, scale.z);
+    const ptglm::M4 Tn = ptglm::transpose4(ptglm::inverse4(T));
+    const ptglm::M4 C = ptglm::mat_mul(T, m.init_inv);
+    const float4* local = (const float4*)m.mem;
+    const float4* init = local + (size_t)m.tri_count * 6;
+    PT_HIP(launch_mesh_refit(local, m.tri_start, m.tri_count, init, ctx->mesh_range[mesh].x, m.node_count, T, Tn, C,
+                             const_cast<float4*>(ctx->scene.tri_geom), const_cast<float4*>(ctx->scene.tri_shade),
+                             const_cast<float4*>(ctx->scene.nodes), ctx->stream));
+    ctx->refitted = true;
+    ctx->resident.reset();  // the resident scene no longer equals its last upload
+    std::memset(ctx->grid, 0, sizeof(ctx->grid));
     return PT_OK;
 }
 

@@ -84,6 +84,17 @@ class Renderer:
         """True: walk the wide BVH records when the scene has them; False: the binary nodes; None: PT_WIDE."""
         check(self._lib.pt_set_wide_walk(self._ctx, -1 if on is None else int(bool(on))), "pt_set_wide_walk")
 
+    def attach_mesh(self, scene: Scene, mesh: int) -> None:
+        """Keep mesh `mesh`'s local triangles and initial boxes on the device for set_mesh_transform."""
+        d = scene.mesh_local(mesh)
+        check(self._lib.pt_mesh_attach(self._ctx, mesh, d["triangles"], d["tri_start"], d["tri_count"], d["init_boxes"],
+                                       d["node_count"], d["init_position"], d["init_scale"]), "pt_mesh_attach")
+
+    def set_mesh_transform(self, mesh: int, position, scale) -> None:
+        """Re-transform an attached mesh and refit its boxes on the device (Bvh/bvh.cpp:332-356)."""
+        check(self._lib.pt_mesh_set_transform(self._ctx, mesh, _abi.Float3(*map(float, position)),
+                                              _abi.Float3(*map(float, scale))), "pt_mesh_set_transform")
+
     def setup_frame(self, width: int, height: int, image_device_ptr: int | None = None) -> None:
         check(self._lib.pt_frame_setup(self._ctx, width, height, C.c_void_p(image_device_ptr or 0)), "pt_frame_setup")
         self.width, self.height = width, height

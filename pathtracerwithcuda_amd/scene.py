@@ -280,6 +280,32 @@ class Scene:
             raise _abi.PtError("scene not built")
         return self._view
 
+    # ---- interactive edits (Core/triangle_mesh.cpp:271-426, Bvh/bvh.cpp:332-356) ----
+    def set_transform(self, mesh: int, position, scale) -> None:
+        """triangle_mesh::set_transform_device + update_bvh: re-transform the mesh and refit its boxes."""
+        check(self._lib.pt_scene_builder_set_transform(self._b, mesh, f3(position), f3(scale)), "set_transform")
+
+    def set_rotate(self, mesh: int, rotate) -> None:
+        check(self._lib.pt_scene_builder_set_rotate(self._b, mesh, f3(rotate)), "set_rotate")
+
+    def apply_rotate(self, mesh: int) -> None:
+        """triangle_mesh::apply_rotate: rotate the mesh-local triangles and rebuild the mesh's BVH."""
+        check(self._lib.pt_scene_builder_apply_rotate(self._b, mesh), "apply_rotate")
+        v = _abi.SceneView()
+        check(self._lib.pt_scene_builder_view(self._b, C.byref(v)), "scene view")  # node arrays moved
+        self._view = v
+
+    def mesh_local(self, mesh: int) -> dict:
+        """Mesh-local triangles, initial boxes and their transform (what Renderer.attach_mesh uploads)."""
+        tris, boxes = C.POINTER(_abi.Triangle)(), C.POINTER(_abi.BoundingBox)()
+        start, count, nodes = C.c_int(), C.c_int(), C.c_int()
+        pos, scl = _abi.Float3(), _abi.Float3()
+        check(self._lib.pt_scene_builder_mesh_local(self._b, mesh, C.byref(tris), C.byref(start), C.byref(count),
+                                                    C.byref(boxes), C.byref(nodes), C.byref(pos), C.byref(scl)),
+              "mesh_local")
+        return {"triangles": tris, "tri_start": start.value, "tri_count": count.value, "init_boxes": boxes,
+                "node_count": nodes.value, "init_position": pos, "init_scale": scl}
+
     def node_count(self) -> int:
         v = self.view
         return sum(v.mesh_node_num[i] for i in range(v.mesh_num))

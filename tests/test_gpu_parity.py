@@ -629,3 +629,45 @@ def test_reference_scene_files(gpu, tmp_path, name, bvh):
     img, img8, ref, ref8, _ = render_both(gpu, sc, cam, cfg, passes=2)
     assert_bitwise(img, ref, f"{name} float")
     assert_bitwise(img8, ref8, f"{name} 8-bit")
+
+
+def test_device_refit_equals_the_edited_scene(require_gpu):
+    """Interactive edits (f4). pt_mesh_set_transform re-transforms an attached mesh's resident triangles
+    and refits its resident boxes on the device (Core/triangle_mesh.cpp:271-328, Bvh/bvh.cpp:332-356);
+    the host builder's set_transform makes the same edit to the reference-layout scene. After each of
+    several moves of two meshes the device-refitted context renders exactly the oracle's image of the
+    edited scene, and exactly what a context given the edited scene by a full upload renders. Then a
+    rotation (apply_rotate: mesh-local rotation + BVH rebuild, re-uploaded) is checked the same way."""
+    sc = pt.cornell_scene(pt.torus_knot(80, 24), cube_length=32)  # meshes: 0 walls, 1 light, 2 knot
+    cfg = pt.configuration(max_tracer_depth=6)
+    cam = pt.camera(64, 40, **BENCH_CAM)
+    r, fresh = pt.Renderer(0), pt.Renderer(0)
+    try:
+        r.upload(sc, cfg)
+        r.attach_mesh(sc, 2)
+        r.attach_mesh(sc, 1)
+        moves = [(2, (0.4, 1.3, -1.2), (0.8, 0.6, 0.7)), (1, (0.2, 2.9, 0.3), (0.6, 0.05, 0.9)),
+                 (2, (-0.9, 0.8, -0.4), (0.5, 0.5, 0.5))]
+        for mesh, pos, scl in moves:
+            r.set_mesh_transform(mesh, pos, scl)
+            sc.set_transform(mesh, pos, scl)
+            r.setup_frame(64, 40)
+            r.render(cam, cfg, 1, 2, write_u8=2)
+            img, img8 = r.download()
+            ref, ref8, _ = oracle.render(sc.view, cam, cfg, 1, 2)
+            assert_bitwise(img.reshape(-1, 3), ref, f"refit mesh {mesh} float")
+            assert_bitwise(img8.reshape(-1, 3), ref8, f"refit mesh {mesh} 8-bit")
+            fresh.upload(sc, cfg)
+            fresh.setup_frame(64, 40)
+            fresh.render(cam, cfg, 1, 2, write_u8=2)
+            assert np.array_equal(fresh.download()[0], img)
+        assert not r.walk_info()["wide_walk"]  # the wide records predate the refit
+        sc.set_rotate(2, (25.0, -40.0, 10.0))
+        sc.apply_rotate(2)
+        r.upload(sc, cfg)
+        img, img8, ref, ref8, _ = render_both(r, sc, cam, cfg, passes=2)
+        assert_bitwise(img, ref, "apply_rotate float")
+        assert_bitwise(img8, ref8, "apply_rotate 8-bit")
+    finally:
+        r.close()
+        fresh.close()

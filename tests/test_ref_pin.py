@@ -119,3 +119,43 @@ def test_png_writer_decodes_with_lodepng(tmp_path, shape, channels):
     np.testing.assert_array_equal(ref[..., :channels], px)
     if channels == 3:
         assert (ref[..., 3] == 255).all()
+
+
+def _triangles(ptr, n):
+    raw = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_ubyte)), (n * C.sizeof(_abi.Triangle),))
+    rec = raw.reshape(n, C.sizeof(_abi.Triangle))
+    v = rec[:, 0:36].copy().view(np.float32).reshape(n, 3, 3)
+    nn = rec[:, 36:72].copy().view(np.float32).reshape(n, 3, 3)
+    return v, nn
+
+
+def _boxes(nodes_ptr, count):
+    raw = np.ctypeslib.as_array(C.cast(nodes_ptr, C.POINTER(C.c_ubyte)), (count * C.sizeof(_abi.BvhNodeDevice),))
+    rec = raw.reshape(count, C.sizeof(_abi.BvhNodeDevice))
+    return rec[:, 0:24].copy().view(np.float32).reshape(count, 6)
+
+
+@pytest.mark.parametrize("moves", [[((0.3, 1.1, -1.4), (0.7, 0.7, 0.7))],
+                                   [((2.0, -0.5, 0.25), (1.3, 0.4, 2.2)), ((-1.0, 0.0, 3.0), (0.05, 0.9, 0.31))]])
+def test_set_transform_refit_matches_glm(moves):
+    """Scene edits (f4): the builder's set_transform — triangles re-transformed from the mesh-local ones,
+    boxes refitted by (transform * initial_transform) — equals set_transform_device + update_bvh run on
+    the reference's glm, bit for bit, after one or several moves."""
+    sc = pt.Scene()
+    sc.add_mesh([pt.torus_knot(40, 12)], [sc.add_material("gold")], position=(0.0, 1.55, -1.5),
+                scale=(0.7, 0.7, 0.7), rotate=(10.0, 20.0, 30.0))
+    sc.build()
+    d = sc.mesh_local(0)
+    n, m = d["tri_count"], d["node_count"]
+    lv, ln = _triangles(d["triangles"], n)
+    init_boxes = _boxes(sc.view.bvh_nodes[0], m)  # the build's boxes = the initial ones
+    ip = (d["init_position"].x, d["init_position"].y, d["init_position"].z)
+    isc = (d["init_scale"].x, d["init_scale"].y, d["init_scale"].z)
+    for pos, scl in moves:
+        sc.set_transform(0, pos, scl)
+        v, nn = _triangles(sc.view.triangles, n)
+        boxes = _boxes(sc.view.bvh_nodes[0], m)
+        rv, rn, rb = oracle.ref_refit(ip, isc, pos, scl, lv.reshape(-1, 3), ln.reshape(-1, 3), init_boxes)
+        assert np.array_equal(v.reshape(-1, 3).view(np.uint32), rv.view(np.uint32))
+        assert np.array_equal(nn.reshape(-1, 3).view(np.uint32), rn.view(np.uint32))
+        assert np.array_equal(boxes.view(np.uint32), rb.view(np.uint32))
