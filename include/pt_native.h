@@ -39,9 +39,9 @@ int pt_scene_upload(pt_context* ctx, int mesh_num, pt_bvh_node_device** bvh_node
 /* Device bytes of the resident scene and its node / triangle counts. */
 int pt_scene_info(pt_context* ctx, long long* device_bytes, int* node_num, int* triangle_num);
 /* The resident scene's wide BVH records (leaf size 1; 0 when the scene's boxes do not allow them) and
- * whether pass_kernel_u walks them (PT_WIDE, default on). DESIGN.md §3.1. */
+ * whether pass_kernel_u walks them (PT_WIDE, default off: measured slower). */
 int pt_scene_walk_info(pt_context* ctx, int* wide_records, int* wide_walk);
-/* 1: walk the wide records when the scene has them, 0: the binary nodes, -1: PT_WIDE (default 1). */
+/* 1: walk the wide records when the scene has them, 0: the binary nodes, -1: PT_WIDE (default 0). */
 int pt_set_wide_walk(pt_context* ctx, int mode);
 
 /* Interactive refit on the device (Core/triangle_mesh.cpp:271-328 + Bvh/bvh.cpp:332-356, which the

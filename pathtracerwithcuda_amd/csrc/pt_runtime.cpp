@@ -654,11 +654,14 @@ bool use_qnodes(const pt_context* ctx) {
     return on && ctx->scene.qnodes != nullptr && !ctx->refitted;
 }
 
-// PT_WIDE=0 keeps pass_kernel_u on the binary nodes even when the scene has wide records.
+// PT_WIDE=1 makes pass_kernel_u walk the wide records when the scene has them. Off by default: exact,
+// 31% fewer lane walk steps, but each step tests all four slots (the SIMD runs every slot some lane
+// needs) and loads 128 B, so the kernel spends 47% more walk cycles: 7066 vs 9974 Mrays/s on the bench
+// frame (profiles/r02/wide/).
 bool use_wide(const pt_context* ctx) {
     static int on = [] {
         const char* e = getenv("PT_WIDE");
-        return e ? atoi(e) != 0 : true;
+        return e ? atoi(e) != 0 : false;
     }();
     const bool want = ctx->wide_mode >= 0 ? ctx->wide_mode != 0 : on;
     return want && ctx->scene.wide != nullptr && !ctx->refitted && !use_qnodes(ctx);

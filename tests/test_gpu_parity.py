@@ -35,17 +35,17 @@ def assert_bitwise(gpu, ref, what=""):
                              f"max |d| {np.nanmax(d):.3g}, mean |d| {np.nanmean(d):.3g}")
 
 
-@pytest.fixture(scope="module", params=["persistent", "persistent_binary", "wavefront"])
+@pytest.fixture(scope="module", params=["persistent", "persistent_wide", "wavefront"])
 def gpu(require_gpu, request):
     """Every parity test runs under both kernel schedules (pt_set_schedule), and the persistent one both
-    with its default walk (the wide BVH records where the scene has them, pt_path.h walk_wide) and on the
-    binary nodes only (pt_set_wide_walk): they must all agree bitwise."""
+    with its default walk (the binary nodes) and walking the wide BVH records where the scene has them
+    (pt_set_wide_walk, pt_path.h walk_wide): they must all agree bitwise."""
     r = pt.Renderer(0)
     sched = "wavefront" if request.param == "wavefront" else "persistent"
     r.set_schedule(sched)
     assert r.schedule() == sched
-    if request.param == "persistent_binary":
-        r.set_wide_walk(False)
+    if request.param == "persistent_wide":
+        r.set_wide_walk(True)
     yield r
     r.close()
 
@@ -363,13 +363,19 @@ def test_schedule_switch_on_one_context(require_gpu):
         r.close()
 
 
-def test_bench_scene_walks_the_wide_records(bench_gpu):
-    """The metric scene gets wide BVH records and the pass kernel walks them by default."""
+def test_bench_scene_has_wide_records(bench_gpu):
+    """The metric scene gets wide BVH records; the pass kernel walks them only when asked (PT_WIDE /
+    pt_set_wide_walk: measured slower)."""
     import bench
     wl = bench.Workload("metric")
     bench_gpu.upload(wl.scene, wl.cfg)
     info = bench_gpu.walk_info()
-    assert info["wide_walk"] and info["wide_records"] > 0
+    assert not info["wide_walk"] and info["wide_records"] > 0
+    bench_gpu.set_wide_walk(True)
+    try:
+        assert bench_gpu.walk_info()["wide_walk"]
+    finally:
+        bench_gpu.set_wide_walk(None)
     leaf3 = pt.cornell_scene(pt.torus_knot(30, 10), cube_length=16, leaf_size=3)
     r = pt.Renderer(0)
     try:
@@ -661,7 +667,9 @@ def test_device_refit_equals_the_edited_scene(require_gpu):
             fresh.setup_frame(64, 40)
             fresh.render(cam, cfg, 1, 2, write_u8=2)
             assert np.array_equal(fresh.download()[0], img)
+        r.set_wide_walk(True)
         assert not r.walk_info()["wide_walk"]  # the wide records predate the refit
+        r.set_wide_walk(None)
         sc.set_rotate(2, (25.0, -40.0, 10.0))
         sc.apply_rotate(2)
         r.upload(sc, cfg)
