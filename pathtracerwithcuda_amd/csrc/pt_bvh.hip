@@ -10,12 +10,15 @@
 //                           (the reference batches on the host, bvh.cpp:920-955)
 //   internal_nodes_kernel   Karras split/range per internal node; parent links resolved with
 //                           atomicMax so the largest writer wins (the reference races here)
-// then the same host second half as the host builder (pt_morton_finish), so the two builders'
-// node arrays are identical.
+// then the second half — bottom-up boxes and the preorder flatten — on the device too (fin_* kernels)
+// for a well-formed tree, or the host builder's own second half (pt_morton_finish) otherwise; either
+// way the two builders' node arrays are identical.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -113,6 +116,125 @@ __global__ __launch_bounds__(kBlock) void reset_parents_kernel(pt_bvh_node_morto
                                                                unsigned int count) {
     const unsigned int i = blockIdx.x * kBlock + threadIdx.x;
     if (i < count) nodes[i].parent_index = -1;
+}
+
+// ---- the second half on the device (bottom-up boxes, preorder flatten) ------------------------------
+// The reference finishes each mesh on the host: every leaf walks to the root unioning boxes (bvh.cpp:
+// 817-860, 974-982), then a stack-based preorder flatten assigns skip indices (:244-330). For a
+// well-formed Karras tree (every node but the root referenced by exactly one internal node — checked
+// by fin_refs/fin_check; otherwise the host finish runs) the same arrays come out of four kernels:
+//   fin_refs      child -> parent links and reference counts (keys: internal i, leaf I + l)
+//   fin_up        one thread per leaf climbs with an arrival counter per internal node: the second
+//                 child to arrive unions the two boxes (left first, as the host fold) and the subtree
+//                 sizes, then climbs on; agent-scope release/acquire around the counter
+//   fin_flatten   each node's preorder position from its path to the root (+1 per ancestor, + the left
+//                 sibling's subtree size when it is a right child); next = position + subtree size;
+//                 a thin leaf box is widened by its parent's box (bvh.cpp:265-268); node records and
+//                 the leaf triangle slots written in place (leaves keep the sorted order in preorder)
+struct FinTree {
+    const pt_bvh_node_morton_code_cuda* inner;   // I internal nodes (children, leaf flags)
+    const pt_bvh_node_morton_code_cuda* leaves;  // L sorted leaves (box, batch id)
+    const int* batch_tris;                       // L * leaf_size triangle ids by batch
+    int* parent;                                 // I + L: the referring internal node
+    int* is_right;                               // I + L: 1 when the node is its parent's right child
+    int* refs;                                   // I + L
+    unsigned int* arrive;                        // I
+    float* inner_box;                            // I * 6
+    int* size;                                   // I + L subtree sizes (leaves 1)
+    int* bad;                                    // set when the tree is not well formed
+    unsigned int I, L;
+};
+
+__device__ __forceinline__ int fin_child_key(const FinTree& t, int index, int is_leaf) {
+    return is_leaf ? (int)t.I + index : index;
+}
+
+__global__ __launch_bounds__(kBlock) void fin_refs_kernel(FinTree t) {
+    const unsigned int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= t.I) return;
+    const pt_bvh_node_morton_code_cuda& n = t.inner[i];
+    const int l = fin_child_key(t, n.left_index, n.is_left_leaf), r = fin_child_key(t, n.right_index, n.is_right_leaf);
+    const int total = (int)(t.I + t.L);
+    if (l < 0 || l >= total || r < 0 || r >= total || l == r) { atomicOr(t.bad, 1); return; }
+    atomicAdd(&t.refs[l], 1);
+    atomicAdd(&t.refs[r], 1);
+    t.parent[l] = (int)i; t.is_right[l] = 0;
+    t.parent[r] = (int)i; t.is_right[r] = 1;
+}
+
+__global__ __launch_bounds__(kBlock) void fin_check_kernel(FinTree t) {
+    const unsigned int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= t.I + t.L) return;
+    if (t.refs[k] != (k == 0 ? 0 : 1)) atomicOr(t.bad, 1);
+}
+
+__device__ __forceinline__ ptbvh::Box fin_box(const FinTree& t, int key) {
+    if (key >= (int)t.I) return to_box(t.leaves[key - (int)t.I].box);
+    const float* b = t.inner_box + (size_t)key * 6;
+    ptbvh::Box r;
+    r.lb[0] = b[0]; r.lb[1] = b[1]; r.lb[2] = b[2]; r.rt[0] = b[3]; r.rt[1] = b[4]; r.rt[2] = b[5];
+    return r;
+}
+
+__global__ __launch_bounds__(kBlock) void fin_up_kernel(FinTree t) {
+    const unsigned int l = blockIdx.x * kBlock + threadIdx.x;
+    if (l >= t.L) return;
+    int key = (int)(t.I + l);
+    t.size[key] = 1;
+    while (key != 0) {
+        const int p = t.parent[key];
+        // publish this subtree's box and size, then arrive; the second arrival finishes the parent
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned int old = atomicAdd(&t.arrive[p], 1u);
+        if (old == 0) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const pt_bvh_node_morton_code_cuda& n = t.inner[p];
+        const int lk = fin_child_key(t, n.left_index, n.is_left_leaf), rk = fin_child_key(t, n.right_index, n.is_right_leaf);
+        ptbvh::Box b = fin_box(t, lk);  // bvh.cpp:837-848: the left child's box expanded by the right's
+        ptbvh::expand(b, fin_box(t, rk));
+        float* o = t.inner_box + (size_t)p * 6;
+        o[0] = b.lb[0]; o[1] = b.lb[1]; o[2] = b.lb[2]; o[3] = b.rt[0]; o[4] = b.rt[1]; o[5] = b.rt[2];
+        t.size[p] = 1 + t.size[lk] + t.size[rk];
+        key = p;
+    }
+}
+
+// pt_bvh_node_device (include/pt_types.h) as the kernel writes it: the leaf slot pointer is the host
+// address the finished array will have
+__global__ __launch_bounds__(kBlock) void fin_flatten_kernel(FinTree t, pt_bvh_node_device* __restrict__ out,
+                                                             int* __restrict__ leaf_slots, int leaf_size,
+                                                             unsigned long long host_leaf_base) {
+    const unsigned int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= t.I + t.L) return;
+    // preorder position: one per ancestor, plus the left sibling's subtree whenever the path turns right
+    int pos = 0;
+    for (int c = (int)k; c != 0;) {
+        const int p = t.parent[c];
+        pos += 1;
+        if (t.is_right[c]) {
+            const pt_bvh_node_morton_code_cuda& n = t.inner[p];
+            pos += t.size[fin_child_key(t, n.left_index, n.is_left_leaf)];
+        }
+        c = p;
+    }
+    const bool leaf = k >= t.I;
+    ptbvh::Box b = fin_box(t, (int)k);
+    if (leaf && ptbvh::is_thin(b)) ptbvh::expand(b, fin_box(t, t.parent[k]));
+    pt_bvh_node_device& d = out[pos];
+    store_box(d.box, b);
+    d.is_leaf = leaf ? 1 : 0;
+    d.next_node_index = pos + t.size[k];
+    if (leaf) {
+        const unsigned int l = k - t.I;
+        const int batch = t.leaves[l].triangle_index;
+        for (int j = 0; j < leaf_size; j++)
+            leaf_slots[(size_t)l * leaf_size + j] = t.batch_tris[(size_t)batch * leaf_size + j];
+        d.triangle_indices = (int*)(host_leaf_base + (unsigned long long)l * leaf_size * sizeof(int));
+    } else {
+        d.triangle_indices = nullptr;
+    }
 }
 
 struct LeafCodes {
@@ -291,6 +413,62 @@ extern "C" int pt_bvh_build_device(const pt_triangle* tris, int n, int start_ind
     int* d_batch = nullptr;
     std::vector<pt_bvh_node_morton_code_cuda> h_leaf(L), h_internal(I);
     t.batch_tris.resize((size_t)L * leaf_size);
+    // PT_BVH_DEVICE_FINISH=0: bottom-up boxes and flattening on the host (pt_morton_finish) as before
+    static const bool device_finish = [] {
+        const char* e = std::getenv("PT_BVH_DEVICE_FINISH");
+        return !(e && std::atoi(e) == 0);
+    }();
+    bool finished = false;
+    void* d_fin = nullptr;
+    pt_bvh_node_device* h_nodes = nullptr;
+    int* h_leaf_idx = nullptr;
+    // the second half on the device (fin_* kernels): false `finished` = the tree is not well formed and
+    // the host finish runs on the downloaded arrays
+    auto finish_on_device = [&]() -> hipError_t {
+        const size_t K = (size_t)I + L, N = K;
+        size_t off = 0;
+        auto take = [&](size_t bytes) { const size_t o = off; off = (off + bytes + 255) & ~(size_t)255; return o; };
+        const size_t o_parent = take(K * 4), o_right = take(K * 4), o_refs = take(K * 4), o_arrive = take((size_t)I * 4),
+                     o_box = take((size_t)I * 24), o_size = take(K * 4), o_bad = take(4),
+                     o_out = take(N * sizeof(pt_bvh_node_device)), o_slots = take((size_t)L * leaf_size * 4);
+        BVH_HIP(hipMalloc(&d_fin, off));
+        uint8_t* base = (uint8_t*)d_fin;
+        BVH_HIP(hipMemsetAsync(base, 0, off, stream));
+        FinTree ft;
+        ft.inner = d_internal;
+        ft.leaves = d_leaf_sorted;
+        ft.batch_tris = d_batch;
+        ft.parent = (int*)(base + o_parent);
+        ft.is_right = (int*)(base + o_right);
+        ft.refs = (int*)(base + o_refs);
+        ft.arrive = (unsigned int*)(base + o_arrive);
+        ft.inner_box = (float*)(base + o_box);
+        ft.size = (int*)(base + o_size);
+        ft.bad = (int*)(base + o_bad);
+        ft.I = I;
+        ft.L = L;
+        hipLaunchKernelGGL(fin_refs_kernel, dim3(grid_of(I)), dim3(kBlock), 0, stream, ft);
+        hipLaunchKernelGGL(fin_check_kernel, dim3(grid_of((unsigned int)K)), dim3(kBlock), 0, stream, ft);
+        BVH_HIP(hipGetLastError());
+        int bad = 0;
+        BVH_HIP(hipMemcpyAsync(&bad, ft.bad, 4, hipMemcpyDeviceToHost, stream));
+        BVH_HIP(hipStreamSynchronize(stream));
+        if (bad) return hipSuccess;  // host finish
+        h_nodes = (pt_bvh_node_device*)std::calloc(N, sizeof(pt_bvh_node_device));
+        h_leaf_idx = (int*)std::malloc((size_t)L * leaf_size * sizeof(int));
+        if (!h_nodes || !h_leaf_idx) return hipErrorOutOfMemory;
+        pt_bvh_node_device* d_out = (pt_bvh_node_device*)(base + o_out);
+        int* d_slots = (int*)(base + o_slots);
+        hipLaunchKernelGGL(fin_up_kernel, dim3(grid_of(L)), dim3(kBlock), 0, stream, ft);
+        hipLaunchKernelGGL(fin_flatten_kernel, dim3(grid_of((unsigned int)K)), dim3(kBlock), 0, stream, ft, d_out, d_slots,
+                           leaf_size, (unsigned long long)(uintptr_t)h_leaf_idx);
+        BVH_HIP(hipGetLastError());
+        BVH_HIP(hipMemcpyAsync(h_nodes, d_out, N * sizeof(pt_bvh_node_device), hipMemcpyDeviceToHost, stream));
+        BVH_HIP(hipMemcpyAsync(h_leaf_idx, d_slots, (size_t)L * leaf_size * sizeof(int), hipMemcpyDeviceToHost, stream));
+        BVH_HIP(hipStreamSynchronize(stream));
+        finished = true;
+        return hipSuccess;
+    };
     auto run = [&]() -> hipError_t {
         BVH_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         BVH_HIP(hipMalloc(&d_tris, sizeof(pt_triangle) * n));
@@ -316,6 +494,10 @@ extern "C" int pt_bvh_build_device(const pt_triangle* tris, int n, int start_ind
             hipLaunchKernelGGL(internal_nodes_kernel, dim3(grid_of(I)), dim3(kBlock), 0, stream, d_internal, I,
                                d_leaf_sorted, L);
             BVH_HIP(hipGetLastError());
+            if (device_finish) {
+                BVH_HIP(finish_on_device());
+                if (finished) return hipSuccess;
+            }
             BVH_HIP(hipMemcpyAsync(h_internal.data(), d_internal, sizeof(pt_bvh_node_morton_code_cuda) * I,
                                    hipMemcpyDeviceToHost, stream));
         }
@@ -326,10 +508,21 @@ extern "C" int pt_bvh_build_device(const pt_triangle* tris, int n, int start_ind
         return hipSuccess;
     };
     const hipError_t e = run();
+    if (d_fin) (void)hipFree(d_fin);
     (void)hipFree(d_tris); (void)hipFree(d_tn); (void)hipFree(d_tn_sorted); (void)hipFree(d_leaf);
     (void)hipFree(d_leaf_sorted); (void)hipFree(d_internal); (void)hipFree(d_mesh); (void)hipFree(d_batch);
     if (stream) (void)hipStreamDestroy(stream);
-    if (e != hipSuccess) return -3;
+    if (e != hipSuccess || !finished) {
+        std::free(h_nodes);
+        std::free(h_leaf_idx);
+        if (e != hipSuccess) return -3;
+    } else {
+        *nodes_out = h_nodes;
+        *node_num_out = (int)(L + I);
+        *leaf_out = h_leaf_idx;
+        *leaf_num_out = (int)L;
+        return 0;
+    }
 
     t.leaf_box.resize(L);
     t.leaf_batch.resize(L);

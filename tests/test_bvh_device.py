@@ -16,7 +16,7 @@ import pytest
 
 import pathtracerwithcuda_amd as pt
 from pathtracerwithcuda_amd import _abi
-from test_bvh import clz, make_tris, morton_py, run_builder
+from test_bvh import build_py, clz, make_tris, morton_py, run_builder
 
 pytestmark = pytest.mark.gpu
 F = np.float32
@@ -68,6 +68,34 @@ def test_device_builder_equals_host_builder(require_gpu, n, leaf, start, kind):
     tris[:5, 0, 0] = F(-0.0) if n > 5 else tris[:5, 0, 0]  # signed zeros in the folds
     got = run_device_builder(tris, start, leaf)
     want = host_as_bytes(tris, start, leaf)
+    assert len(got) == len(want)
+    assert got == want
+
+
+def py_as_bytes(tris, start, leaf_size):
+    out = []
+    for lb, rt, is_leaf, nxt, slots in build_py(tris, start, leaf_size):
+        box = _abi.BoundingBox(_abi.Float3(*map(float, lb)), _abi.Float3(*map(float, rt)),
+                               _abi.Float3(*map(float, (F(0.5) * (rt + lb)).astype(F))))
+        out.append((bytes(box), is_leaf, nxt, slots))
+    return out
+
+
+@pytest.mark.parametrize("n,leaf,start,kind", [(2, 1, 0, "rand"), (300, 1, 0, "rand"), (301, 2, 10, "rand"),
+                                               (1000, 4, 3, "rand"), (200, 1, 0, "flat"), (6000, 1, 5, "rand"), (40000, 1, 0, "rand"),
+                                               (120, 1, 0, "dup")])
+def test_device_builder_equals_python_restatement(require_gpu, n, leaf, start, kind):
+    """Row f1 with the second half on the device (bottom-up boxes by arrival counters, preorder flatten,
+    pt_bvh.hip fin_*): the node array equals tests/test_bvh.py::build_py — the independent Python
+    restatement of bvh.cpp:862-1047 + :244-330 — byte for byte (boxes with centroids, leaf flags, skip
+    indices, leaf triangle slots). The duplicate-code case may be a malformed tree, for which the host
+    finish runs instead; the result must be the same either way."""
+    if kind == "dup":
+        tris = np.repeat(make_tris(3, 1), n // 3, axis=0)
+    else:
+        tris = make_tris(n, n * 11 + leaf, kind == "flat")
+    got = run_device_builder(tris, start, leaf)
+    want = py_as_bytes(tris, start, leaf)
     assert len(got) == len(want)
     assert got == want
 

@@ -1,5 +1,7 @@
 """Host vs GPU Morton BVH build time (row f1) on the benchmark mesh sizes: 70k (config 2) and
-800k (config 4) torus-knot triangles. Prints one JSON line per size; run on the GPU box."""
+800k (config 4) torus-knot triangles. Prints one JSON line per size; run on the GPU box.
+PT_BVH_DEVICE_FINISH=0 times the device builder with its second half (bottom-up boxes, flatten) on the
+host, as in round 1; the default runs it on the device (pt_bvh.hip fin_* kernels)."""
 import ctypes as C
 import json
 import os
@@ -50,4 +52,5 @@ for tub, rad in ((350, 100), (1000, 400)):
         if dev:
             build()  # warm-up: HIP runtime, code object load
         out[name + "_ms"] = round(timed(build) * 1000, 2)
-    print(json.dumps({"triangles": n, **out}), flush=True)
+    fin = "host" if os.environ.get("PT_BVH_DEVICE_FINISH", "1") == "0" else "device"
+    print(json.dumps({"triangles": n, **out, "device_second_half_on": fin}), flush=True)
