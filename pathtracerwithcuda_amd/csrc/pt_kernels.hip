@@ -260,7 +260,7 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
 // PROF: wave-level occupancy counters of the state machine into stats[16..23] (tools/uprof.py):
 // rounds, walk steps, walking lanes summed over steps, shading batches, lanes shaded, triangle
 // batches, lanes in triangle batches, lanes refilled.
-template <int MINW, bool PROF, bool QN, int CHAIN, bool PF, bool WIDE>
+template <int MINW, bool PROF, bool QN, int CHAIN, bool PF, bool WIDE, int FEAT = PT_FEAT_ALL>
 __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
                                                                 int walk_steps, int tri_min, int walk_min, int tail) {
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     bool a2 = shade_hit<false>(sc, cfg, d2, pseed, &p2, h2, &none);
                     opaque(p2); opaque(a2);
                 }
-                alive = shade_hit<false>(sc, cfg, depth, pseed, &ps, h, &none, PROF ? prof + 11 : nullptr);
+                alive = shade_hit<false, FEAT>(sc, cfg, depth, pseed, &ps, h, &none, PROF ? prof + 11 : nullptr);
             }
             if (PROF) tc2 = __builtin_readcyclecounter();
             if (mode == LANE_READY) {  // the pass's end for this unit, or the next trace step
@@ -719,9 +719,31 @@ bool unified_enabled() {
 
 using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int, int, int);
 
+// The product configuration specialised on the scene's features (pt_path.h PT_FEAT_*): feat is what the
+// scene can reach; PT_FEAT_SPECIALISE=0 keeps the all-features kernel.
+static PassFnU pass_fn_feat(int minw, int feat) {
+    static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
+    if (!spec) feat = PT_FEAT_ALL;
+    switch (minw * 4 + feat) {
+        case 5 * 4 + 0: return pass_kernel_u<5, false, false, 2, true, false, 0>;
+        case 5 * 4 + 1: return pass_kernel_u<5, false, false, 2, true, false, 1>;
+        case 5 * 4 + 2: return pass_kernel_u<5, false, false, 2, true, false, 2>;
+        case 6 * 4 + 0: return pass_kernel_u<6, false, false, 2, true, false, 0>;
+        case 6 * 4 + 1: return pass_kernel_u<6, false, false, 2, true, false, 1>;
+        case 6 * 4 + 2: return pass_kernel_u<6, false, false, 2, true, false, 2>;
+        case 7 * 4 + 0: return pass_kernel_u<7, false, false, 2, true, false, 0>;
+        case 7 * 4 + 1: return pass_kernel_u<7, false, false, 2, true, false, 1>;
+        case 7 * 4 + 2: return pass_kernel_u<7, false, false, 2, true, false, 2>;
+        case 8 * 4 + 0: return pass_kernel_u<8, false, false, 2, true, false, 0>;
+        case 8 * 4 + 1: return pass_kernel_u<8, false, false, 2, true, false, 1>;
+        default: break;
+    }
+    return nullptr;
+}
+
 // PT_WALK_CHAIN: records per binary walk step (walk_box_chain); 1 = walk_box. wide: the scene has wide
-// records and PT_WIDE (default 1) allows their walk (walk_wide).
-static PassFnU pass_fn_u(int minw, bool qn, bool wide) {
+// records and PT_WIDE (default 0) allows their walk (walk_wide). feat: the scene's reachable features.
+static PassFnU pass_fn_u(int minw, bool qn, bool wide, int feat) {
     static const int prof = env_int("PT_UPROF", 0, 0, 1);
     static const int chain = env_int("PT_WALK_CHAIN", 2, 1, 3);
     static const int pf = env_int("PT_TRI_PREFETCH", 1, 0, 1);
@@ -731,6 +753,10 @@ static PassFnU pass_fn_u(int minw, bool qn, bool wide) {
     if (wide) return minw == 5 ? pass_kernel_u<5, false, false, 2, true, true> : pass_kernel_u<6, false, false, 2, true, true>;
     if (chain == 1) return minw == 6 ? pass_kernel_u<6, false, false, 1, false, false> : pass_kernel_u<5, false, false, 1, false, false>;
     if (chain == 3) return minw == 6 ? pass_kernel_u<6, false, false, 3, false, false> : pass_kernel_u<5, false, false, 3, false, false>;
+    if (pf && feat != PT_FEAT_ALL) {
+        PassFnU f = pass_fn_feat(minw, feat);
+        if (f) return f;
+    }
     if (pf) return minw == 7 ? pass_kernel_u<7, false, false, 2, true, false>
                              : (minw == 6 ? pass_kernel_u<6, false, false, 2, true, false> : pass_kernel_u<5, false, false, 2, true, false>);
     return minw == 6 ? pass_kernel_u<6, false, false, 2, false, false> : pass_kernel_u<5, false, false, 2, false, false>;
@@ -744,8 +770,8 @@ static bool use_unified(bool leaf1, bool stats, bool qn, int lds_bytes) {
     return leaf1 && !stats && unified_enabled() && lds_bytes <= PT_LDS_TABLES;
 }
 
-hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, bool wide, int first_pass, int batch_log2,
-                       int write_u8, int grid, bool stats, int lds_bytes, hipStream_t stream) {
+hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, bool wide, int feat, int first_pass,
+                       int batch_log2, int write_u8, int grid, bool stats, int lds_bytes, hipStream_t stream) {
     if (use_unified(leaf1, stats, qn, lds_bytes)) {
         // 64-unit chunks and a 28-lane shading batch: measured best with frames in flight
         static const int chunk = env_int("PT_CHUNK_MEGA", 64, 0, 4096);
@@ -760,7 +786,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, bool
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
             a8 = walk_min, a9 = tail_shade | (tail_walk << 8);
         void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8, &a9};
-        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn, wide && !qn), dim3(grid), dim3(PT_UBLOCK), args,
+        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn, wide && !qn, feat), dim3(grid), dim3(PT_UBLOCK), args,
                                        (size_t)lds_bytes, stream);
         if (e != hipSuccess) return e;
         return hipGetLastError();
@@ -791,12 +817,12 @@ hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256
     return hipGetLastError();
 }
 
-int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int lds_bytes) {
+int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int feat, int lds_bytes) {
     int dev = 0, cus = 0, blocks = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const bool u = use_unified(leaf1, stats, qn, lds_bytes);
-    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true), qn, wide && !qn)
+    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true), qn, wide && !qn, feat)
                        : (const void*)pass_fn(leaf1, stats, pass_min_waves(false), qn);
     const size_t lds = u ? (size_t)lds_bytes : 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, u ? PT_UBLOCK : PT_BLOCK, lds) != hipSuccess || blocks <= 0) blocks = u ? 4 * PT_BLOCK / PT_UBLOCK : 4;

@@ -739,7 +739,16 @@ __device__ __forceinline__ Hit closest_hit(const DevScene& sc, v3 o, v3 d, Count
 // The per-path part of the trace seed hash(seed) * hash(pixel) * hash(depth) (:415), int wrap.
 __device__ __forceinline__ int32_t path_seed(int32_t hseed, int pixel) { return mul_wrap(hseed, hash_pt(pixel)); }
 
-template <bool STATS>
+// Scene features shade_hit can meet (pass_kernel_u is specialised on them: code a scene cannot reach is
+// left out, which lowers the kernel's register peak). A feature left out must be unreachable for the
+// scene: PT_FEAT_MEDIUM when no material (and not the configured air) has an absorption or reduced
+// scattering coefficient other than 0 — the medium step is then never taken (:456-492); PT_FEAT_TEX when
+// no material has a texture (:518-526).
+#define PT_FEAT_MEDIUM 1
+#define PT_FEAT_TEX 2
+#define PT_FEAT_ALL 3
+
+template <bool STATS, int FEAT = PT_FEAT_ALL>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
                                           PathState* ps, const Hit& h, Counters* ctr, unsigned long long* pc = nullptr);
 
@@ -757,7 +766,7 @@ __device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& 
 // Fresnel-selected bounce, accumulation, kill test.
 // pc (PT_UPROF builds): cycles spent per phase, added into pc[0..3] (medium, hit record or miss,
 // Fresnel, bounce).
-template <bool STATS>
+template <bool STATS, int FEAT>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
                                           PathState* ps, const Hit& h, Counters* ctr, unsigned long long* pc) {
     unsigned long long tq = pc ? __builtin_readcyclecounter() : 0;
@@ -770,7 +779,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
     // medium: absorption and subsurface scattering (:456-492). A scattering lane replaces its ray in
     // place, and the rest of the step reads the ray back from *ps afterwards (below), so the
     // replaced and the original ray share registers instead of both living through the shading.
-    {
+    if (FEAT & PT_FEAT_MEDIUM) {
         float sa[3], ss[3];
         medium_coefficients(sc, cfg, ps->medium, sa, ss);
         if (ss[0] > 0.0f || length(mk3(sa[0], sa[1], sa[2])) > cfg.sss_threshold) {
@@ -818,7 +827,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
         float w = 1.0f - h.t1 - h.t2;
         normal = n0 * w + n1 * h.t1 + n2 * h.t2;
         const DevMaterial& M = sc.materials[mid];
-        if (M.diffuse_texture_id != -1 || M.specular_texture_id != -1) {
+        if ((FEAT & PT_FEAT_TEX) && (M.diffuse_texture_id != -1 || M.specular_texture_id != -1)) {
             float4 s3 = sh[3];
             v2 uv0 = mk2(s2.y, s2.z), uv1 = mk2(s2.w, s3.x), uv2 = mk2(s3.y, s3.z);
             uv = uv0 * w + uv1 * h.t1 + uv2 * h.t2;

@@ -450,6 +450,7 @@ struct pt_context {
     int node_num = 0, tri_num = 0, wide_num = 0;
     bool has_scene = false;
     int material_num = 0;
+    int scene_feat = PT_FEAT_ALL;  // features the resident scene's materials can reach (pt_path.h PT_FEAT_*)
     float mat_air_n = 0.0f;       // air index the per-material constants were computed for
     bool mat_air_n_valid = false;
     // frame
@@ -466,7 +467,7 @@ struct pt_context {
     bool instrumented = false;
     int schedule = -1;  // PT_SCHEDULE_*; -1: environment default (PT_MODE)
     int wide_mode = -1; // pass_kernel_u walks the wide records: 1 on, 0 off, -1 environment default (PT_WIDE)
-    int grid[2][2][3] = {};
+    int grid[2][2][3][4] = {};
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
     size_t ev_used = 0;
@@ -596,6 +597,12 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     ctx->tri_num = (int)(st.tri_geom.size() / 3);
     ctx->material_num = (int)st.mats.size();
     ctx->mat_air_n_valid = false;
+    ctx->scene_feat = 0;
+    for (const DevMaterial& m : st.mats) {
+        if (m.diffuse_texture_id != -1 || m.specular_texture_id != -1) ctx->scene_feat |= PT_FEAT_TEX;
+        for (int c = 0; c < 3; c++)
+            if (m.absorption[c] != 0.0f || m.reduced_scattering[c] != 0.0f) ctx->scene_feat |= PT_FEAT_MEDIUM;
+    }
     ctx->has_scene = true;
     std::memset(ctx->grid, 0, sizeof(ctx->grid));  // occupancy depends on the LDS material table
     return PT_OK;
@@ -672,11 +679,20 @@ int pass_lds_bytes(const pt_context* ctx) {
     return ctx->material_num * (int)sizeof(DevMaterial) + ctx->scene.sphere_num * 32;
 }
 
-int pass_grid(pt_context* ctx) {
+// The features a render can reach: the scene's, plus a participating medium when the configured air
+// scatters or absorbs (shade_hit's medium step runs for air paths then).
+int render_feat(const pt_context* ctx, const DevConfig& dc) {
+    int f = ctx->scene_feat;
+    for (int c = 0; c < 3; c++)
+        if (dc.air_absorption[c] != 0.0f || dc.air_reduced_scattering[c] != 0.0f) f |= PT_FEAT_MEDIUM;
+    return f;
+}
+
+int pass_grid(pt_context* ctx, int feat) {
     const bool leaf1 = ctx->scene.leaf_size == 1, qn = use_qnodes(ctx), wide = use_wide(ctx);
-    int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0][qn ? 1 : (wide ? 2 : 0)];
+    int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0][qn ? 1 : (wide ? 2 : 0)][feat & 3];
     if (g == 0) {
-        g = pass_grid_size(leaf1, ctx->instrumented, qn, wide, pass_lds_bytes(ctx));
+        g = pass_grid_size(leaf1, ctx->instrumented, qn, wide, feat, pass_lds_bytes(ctx));
         // PT_GRID_PCT: experiment knob, a percentage of the occupancy-sized grid
         const char* e = getenv("PT_GRID_PCT");
         const int pct = e ? atoi(e) : 100;
@@ -821,7 +837,8 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     }
     // Single-kernel schedule: up to max_pass_batch() passes per launch (pt_kernels.hip pass_kernel),
     // a power of two so a unit splits into (pixel, pass) by shift and mask.
-    const int grid = pass_grid(ctx);
+    const int feat = render_feat(ctx, dc);
+    const int grid = pass_grid(ctx, feat);
     const int units = ctx->tiling.unit_count;
     int most = 1;
     while (most * 2 <= max_pass_batch() && (long long)units * most * 2 <= (1ll << 28)) most *= 2;
@@ -846,7 +863,7 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
         int rc = ev_begin(ctx, 0);
         if (rc != PT_OK) return rc;
-        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, use_qnodes(ctx), use_wide(ctx), first, lg, w8, grid,
+        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, use_qnodes(ctx), use_wide(ctx), feat, first, lg, w8, grid,
                            ctx->instrumented, pass_lds_bytes(ctx), ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         if (lg > 0) {
