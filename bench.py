@@ -314,9 +314,7 @@ def main() -> int:
         # one launch = a batch of passes over the frame (this rank's bands when tiled)
         bytes_per_launch = algorithmic_bytes(counts, scene.view.sphere_num, cfg.bvh_leaf_node_triangle_num,
                                              width * height, spp) / world / launches_per_frame
-        kernel_name = (f"pass_kernel_u<MINW={os.environ.get('PT_MIN_WAVES', '6')},"
-                       f"CHAIN={os.environ.get('PT_WALK_CHAIN', '2')},PF={os.environ.get('PT_TRI_PREFETCH', '1')}>"
-                       if os.environ.get("PT_UNIFIED", "1") != "0" else "pass_kernel<LEAF1=true,STATS=false,MINW=8>")
+        kernel_name = r.last_kernel()
     else:
         # one launch = one depth of one pass
         bytes_per_launch = extend_bytes(counts, scene.view.sphere_num) / world / launches_per_frame

@@ -43,6 +43,8 @@ int pt_scene_info(pt_context* ctx, long long* device_bytes, int* node_num, int* 
 int pt_scene_walk_info(pt_context* ctx, int* wide_records, int* wide_walk);
 /* 1: walk the wide records when the scene has them, 0: the binary nodes, -1: PT_WIDE (default 0). */
 int pt_set_wide_walk(pt_context* ctx, int mode);
+/* The pass kernel (and its template configuration) the last render call of this context launched. */
+const char* pt_last_kernel(pt_context* ctx);
 
 /* Interactive refit on the device (Core/triangle_mesh.cpp:271-328 + Bvh/bvh.cpp:332-356, which the
  * reference runs on the host over managed memory). pt_mesh_attach keeps mesh `mesh`'s mesh-local

@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <string>
+
 #include "pt_glm.h"
 #include "pt_path.h"
 #include "pt_work.h"
@@ -25,7 +27,8 @@ int shade_grid_waves();
 hipError_t launch_finalize(const LaunchParams* P, int units, int pass, int write_u8, int traced, hipStream_t s);
 hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256, int pixel_count, int pass,
                      hipStream_t stream);
-int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int feat, int lds_bytes);  // lds_bytes: pass_kernel_u's dynamic LDS
+int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int feat, int lds_bytes);
+std::string pass_kernel_desc(bool leaf1, bool stats, bool qn, bool wide, int feat, int lds_bytes);  // lds_bytes: pass_kernel_u's dynamic LDS
 int env_int(const char* name, int dflt, int lo, int hi);  // clamped integer from the environment
 hipError_t launch_material_consts(DevMaterial* mats, int n, float air_n, hipStream_t stream);
 hipError_t launch_mesh_refit(const float4* local, int tri_start, int tri_count, const float4* init_nodes, int node_first,

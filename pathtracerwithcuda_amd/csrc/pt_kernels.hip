@@ -13,7 +13,9 @@
 // (stable remove_if of dead pixels) done in-register, per wave, with no host synchronisation.
 // Results do not depend on the schedule: every random draw is seeded by (pass, pixel, depth)
 // (path_tracer_kernel.cu:324,415) and a pixel's passes are ordered by the launch sequence.
+#include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #include "pt_kernels.h"
 
@@ -699,15 +701,18 @@ static PassFn pass_fn(bool leaf1, bool stats, int minw, bool qn) {
     return pass_kernel<false, true, 5, false>;
 }
 
-// PT_MIN_WAVES overrides the occupancy target: 8 waves/SIMD for pass_kernel (64 VGPRs), 6 for
-// pass_kernel_u (80 VGPRs, a few spilled), the measured optimum of each.
-int pass_min_waves(bool unified) {
+// PT_MIN_WAVES overrides the occupancy target: 8 waves/SIMD for pass_kernel (64 VGPRs); for pass_kernel_u
+// 7 when the scene reaches neither textures nor media (72 VGPRs, no spills: +3.5% over 6 on the bench
+// frame, profiles/r02/feat1) and 6 otherwise (80 VGPRs; at 72 the full kernel spills and loses 5%).
+int pass_min_waves(bool unified, int feat) {
     static int w = [] {
         const char* e = getenv("PT_MIN_WAVES");
         int v = e ? atoi(e) : 0;
         return (v >= 4 && v <= 8) ? v : 0;
     }();
-    return w ? w : (unified ? 6 : 8);
+    if (w) return w;
+    if (!unified) return 8;
+    return feat == 0 ? 7 : 6;
 }
 
 // PT_UNIFIED=0 selects pass_kernel for the default configuration (leaf size 1, uninstrumented, exact
@@ -786,12 +791,12 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, bool
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
             a8 = walk_min, a9 = tail_shade | (tail_walk << 8);
         void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8, &a9};
-        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true), qn, wide && !qn, feat), dim3(grid), dim3(PT_UBLOCK), args,
+        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true, feat), qn, wide && !qn, feat), dim3(grid), dim3(PT_UBLOCK), args,
                                        (size_t)lds_bytes, stream);
         if (e != hipSuccess) return e;
         return hipGetLastError();
     }
-    PassFn fn = pass_fn(leaf1, stats, pass_min_waves(false), qn);
+    PassFn fn = pass_fn(leaf1, stats, pass_min_waves(false, feat), qn);
     const LaunchParams* a0 = params_dev;
     static const int chunk = env_int("PT_CHUNK_MEGA", 32, 0, 4096);
     int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2;
@@ -817,13 +822,30 @@ hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256
     return hipGetLastError();
 }
 
+// The pass kernel launch_pass picks for these arguments, as text (bench.py's roofline.kernel).
+std::string pass_kernel_desc(bool leaf1, bool stats, bool qn, bool wide, int feat, int lds_bytes) {
+    char buf[160];
+    if (use_unified(leaf1, stats, qn, lds_bytes)) {
+        static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
+        static const int chain = env_int("PT_WALK_CHAIN", 2, 1, 3);
+        static const int pf = env_int("PT_TRI_PREFETCH", 1, 0, 1);
+        std::snprintf(buf, sizeof(buf), "pass_kernel_u<MINW=%d,QN=%d,CHAIN=%d,PF=%d,WIDE=%d,FEAT=%d>",
+                      pass_min_waves(true, feat), qn ? 1 : 0, qn ? 1 : chain, qn ? 0 : pf, wide && !qn ? 1 : 0,
+                      spec && !qn && !wide && pf && chain == 2 ? feat : PT_FEAT_ALL);
+    } else {
+        std::snprintf(buf, sizeof(buf), "pass_kernel<LEAF1=%d,STATS=%d,MINW=%d,QN=%d>", leaf1 ? 1 : 0, stats ? 1 : 0,
+                      pass_min_waves(false, feat), qn ? 1 : 0);
+    }
+    return buf;
+}
+
 int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int feat, int lds_bytes) {
     int dev = 0, cus = 0, blocks = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const bool u = use_unified(leaf1, stats, qn, lds_bytes);
-    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true), qn, wide && !qn, feat)
-                       : (const void*)pass_fn(leaf1, stats, pass_min_waves(false), qn);
+    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true, feat), qn, wide && !qn, feat)
+                       : (const void*)pass_fn(leaf1, stats, pass_min_waves(false, feat), qn);
     const size_t lds = u ? (size_t)lds_bytes : 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, u ? PT_UBLOCK : PT_BLOCK, lds) != hipSuccess || blocks <= 0) blocks = u ? 4 * PT_BLOCK / PT_UBLOCK : 4;
     if (cus <= 0) cus = 256;

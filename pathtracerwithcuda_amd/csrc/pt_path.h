@@ -505,10 +505,31 @@ __device__ __forceinline__ bool chain_test(const ChainRecs<CHAIN>& r, v3 o, v3 i
     }
     return false;
 }
+#ifndef PT_CHAIN_FLAT
+#define PT_CHAIN_FLAT 0
+#endif
+// chain_test for two records without branches (PT_CHAIN_FLAT builds): both boxes are tested, then the
+// outcome of the two-record walk is selected. The second record's test is only USED when the first
+// node is an internal node that passes, exactly when chain_test would run it; the lanes' visited
+// nodes and accepted tests are unchanged.
+__device__ __forceinline__ bool chain_test_flat2(const ChainRecs<2>& r, v3 o, v3 inv, MeshWalk& w, int& tri) {
+    float e0, e1;
+    const bool h0 = box_hit(r.lo[0], r.hi[0], o, inv, &e0) & (e0 <= w.t);
+    const bool h1 = box_hit(r.lo[1], r.hi[1], o, inv, &e1) & (e1 <= w.t);
+    const int s0 = f2i(r.hi[0].w), s1 = f2i(r.hi[1].w);
+    const bool leaf0 = s0 >= 0, leaf1 = s1 >= 0;
+    const bool parked = h0 & (leaf0 | (h1 & leaf1));
+    tri = leaf0 ? s0 : s1;
+    const int skip0 = f2i(r.lo[0].w), skip1 = f2i(r.lo[1].w);
+    w.pos = !h0 ? skip0 : (leaf0 ? w.pos : (!h1 ? skip1 : (leaf1 ? w.pos + 1 : w.pos + 2)));
+    return parked;
+}
+
 template <int CHAIN>
 __device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri) {
     ChainRecs<CHAIN> r;
     chain_load<CHAIN>(rn, w.pos, r);
+    if constexpr (CHAIN == 2 && PT_CHAIN_FLAT) return chain_test_flat2(r, o, inv, w, tri);
     return chain_test<CHAIN>(r, o, inv, w, tri);
 }
 

@@ -450,7 +450,8 @@ struct pt_context {
     int node_num = 0, tri_num = 0, wide_num = 0;
     bool has_scene = false;
     int material_num = 0;
-    int scene_feat = PT_FEAT_ALL;  // features the resident scene's materials can reach (pt_path.h PT_FEAT_*)
+    int scene_feat = PT_FEAT_ALL;
+    std::string last_kernel;       // the pass kernel of the last render (pt_last_kernel)  // features the resident scene's materials can reach (pt_path.h PT_FEAT_*)
     float mat_air_n = 0.0f;       // air index the per-material constants were computed for
     bool mat_air_n_valid = false;
     // frame
@@ -839,6 +840,8 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     // a power of two so a unit splits into (pixel, pass) by shift and mask.
     const int feat = render_feat(ctx, dc);
     const int grid = pass_grid(ctx, feat);
+    ctx->last_kernel = pass_kernel_desc(ctx->scene.leaf_size == 1, ctx->instrumented, use_qnodes(ctx), use_wide(ctx),
+                                        feat, pass_lds_bytes(ctx));
     const int units = ctx->tiling.unit_count;
     int most = 1;
     while (most * 2 <= max_pass_batch() && (long long)units * most * 2 <= (1ll << 28)) most *= 2;
@@ -1058,6 +1061,8 @@ extern "C" int pt_mesh_set_transform(pt_context* ctx, int mesh, pt_float3 positi
     std::memset(ctx->grid, 0, sizeof(ctx->grid));
     return PT_OK;
 }
+
+extern "C" const char* pt_last_kernel(pt_context* ctx) { return ctx ? ctx->last_kernel.c_str() : ""; }
 
 extern "C" int pt_scene_walk_info(pt_context* ctx, int* wide_records, int* wide_walk) {
     if (!ctx) return PT_E_ARG;

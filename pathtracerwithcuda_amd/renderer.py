@@ -74,6 +74,11 @@ class Renderer:
         check(self._lib.pt_scene_info(self._ctx, C.byref(b), C.byref(n), C.byref(t)), "pt_scene_info")
         return {"device_bytes": b.value, "nodes": n.value, "triangles": t.value}
 
+    def last_kernel(self) -> str:
+        """The pass kernel configuration the last render launched (e.g. pass_kernel_u<MINW=7,...>)."""
+        v = self._lib.pt_last_kernel(self._ctx)
+        return v.decode() if v else ""
+
     def walk_info(self) -> dict:
         """Wide BVH records of the resident scene and whether the pass kernel walks them."""
         n, on = C.c_int(), C.c_int()
