@@ -43,6 +43,9 @@ int pt_scene_info(pt_context* ctx, long long* device_bytes, int* node_num, int* 
 int pt_scene_walk_info(pt_context* ctx, int* wide_records, int* wide_walk);
 /* 1: walk the wide records when the scene has them, 0: the binary nodes, -1: PT_WIDE (default 0). */
 int pt_set_wide_walk(pt_context* ctx, int mode);
+/* 1: run the pass as walker waves and shader waves that regroup paths through LDS (pass_kernel_r),
+ * 0: every wave walks and shades (pass_kernel_u), -1: PT_REGROUP (default 0). Same results either way. */
+int pt_set_regroup(pt_context* ctx, int mode);
 /* The pass kernel (and its template configuration) the last render call of this context launched. */
 const char* pt_last_kernel(pt_context* ctx);
 

@@ -474,6 +474,337 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     }
 }
 
+// ---- pass_kernel_r: walker waves and shader waves regrouping paths through LDS ------------------
+// In pass_kernel_u every wave both walks and shades, so a wave shades whatever subset of its lanes is
+// ready (about 40 of 64 on the bench frame) and walks with the lanes that are not. Here a workgroup's
+// waves take fixed roles. NWALK walker waves only walk: a lane whose closest hit is known hands its
+// path (state and hit) to a slot of its wave's partition of PT_RG_PART LDS slots and takes a path
+// that waits there for its next segment (a swap through one slot), or a new (pixel, pass) unit.
+// NSHADE shader waves only shade: shader k serves the slots s with s % NSHADE == k, takes up to 64
+// waiting paths at a time (shade_min of them, or fewer once it has waited rg_spin rounds), runs
+// shade_hit on them, and writes a surviving path back into its slot for the walkers, or finishes
+// the unit. Every path still computes exactly the reference sequence: the same walk, the same shade,
+// the same draws keyed by (pass, pixel, depth); only the lane that runs each step changes.
+//
+// Slot ownership makes the exchange lock-free: a FREE or WALK slot belongs to its walker wave, a
+// SHADE slot to its shader wave, and only the owner moves a slot to the next state, after its data
+// stores have completed (s_waitcnt lgkmcnt(0) between the data and the state store; readers load the
+// state first). A walker wave exits once the work is drained, none of its lanes holds a path and its
+// partition is all FREE; the shader waves exit once every walker wave has exited.
+#define PT_RG_PART 64
+#define PT_RG_IDLE_CAP (1 << 24)  // idle rounds after which a wave gives up (never reached by a correct run)
+enum : int { SLOT_FREE = 0, SLOT_WALK = 1, SLOT_SHADE = 2 };
+enum : int { LANE_NEW = 5 };  // walker lane holding a path that starts its next segment
+
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// q0 (o, d.x) q1 (d.y, d.z, thr.x, thr.y) q2 (thr.z, rad) q3 (unit, pseed, medium, depth) q4 (hit)
+__device__ __forceinline__ void slot_put(float4* const q[5], int s, const PathState& ps, unsigned int unit, int32_t pseed,
+                                         int depth, const Hit* h) {
+    q[0][s] = make_float4(ps.o.x, ps.o.y, ps.o.z, ps.d.x);
+    q[1][s] = make_float4(ps.d.y, ps.d.z, ps.thr.x, ps.thr.y);
+    q[2][s] = make_float4(ps.thr.z, ps.rad.x, ps.rad.y, ps.rad.z);
+    q[3][s] = make_float4(__uint_as_float(unit), __int_as_float(pseed), __int_as_float(ps.medium), __int_as_float(depth));
+    if (h) q[4][s] = make_float4(h->t, h->t1, h->t2, __int_as_float(h->prim * 4 + h->type));
+}
+
+__device__ __forceinline__ void slot_get(float4* const q[5], int s, PathState& ps, unsigned int& unit, int32_t& pseed,
+                                         int& depth, Hit* h) {
+    const float4 a = q[0][s], b = q[1][s], c = q[2][s], e = q[3][s];
+    ps.o = mk3(a.x, a.y, a.z);
+    ps.d = mk3(a.w, b.x, b.y);
+    ps.thr = mk3(b.z, b.w, c.x);
+    ps.rad = mk3(c.y, c.z, c.w);
+    unit = __float_as_uint(e.x); pseed = __float_as_int(e.y); ps.medium = __float_as_int(e.z); depth = __float_as_int(e.w);
+    if (h) {
+        const float4 f = q[4][s];
+        const int pt = __float_as_int(f.w);
+        h->t = f.x; h->t1 = f.y; h->t2 = f.z; h->type = pt & 3; h->prim = pt >> 2;
+    }
+}
+
+// PROF counters (stats[16..], tools/rgprof.py): walker rounds, handoffs, lanes handed to shading, walk
+// steps, walking lanes summed over steps, walker idle rounds, shader batches, lanes shaded, shader idle
+// rounds, triangle batches, then cycles: walker handoff, walker walk, walker idle, shader shading,
+// shader idle, lanes in triangle batches.
+template <int MINW, int NWALK, int NSHADE, bool PROF, int FEAT>
+__global__ __launch_bounds__((NWALK + NSHADE) * 64, MINW) void pass_kernel_r(
+    const LaunchParams* __restrict__ params, int first_pass, int write_u8, int chunk, int batch_log2, int shade_min,
+    int walk_steps, int tri_min, int walk_min, int rg) {
+    constexpr int NT = (NWALK + NSHADE) * 64;
+    constexpr int S = NWALK * PT_RG_PART;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const LaunchParams* P0 = params;
+    const float clamp_hi = (float)P0->cfg.max_depth * 2.0f;
+    const unsigned long long below = lanes_below(lane);
+    __shared__ int2 lds_mesh[PT_LDS_MESHES];
+    __shared__ float4 slot_q[5][S];
+    __shared__ int slot_state[S];
+    __shared__ int scratch[NWALK + NSHADE][128];
+    __shared__ int walkers_done;
+    extern __shared__ float4 lds_dyn[];
+    DevMaterial* lds_mats = reinterpret_cast<DevMaterial*>(lds_dyn);
+    {
+        const int2* mr = uniform_ptr(P0->sc.mesh_range);
+        const int n = min(uniform_int(P0->sc.mesh_num), PT_LDS_MESHES);
+        for (int i = threadIdx.x; i < n; i += NT) lds_mesh[i] = mr[i];
+        const float4* ms = reinterpret_cast<const float4*>(uniform_ptr(P0->sc.materials));
+        const int nm = uniform_int(P0->sc.material_num) * (int)(sizeof(DevMaterial) / 16);
+        for (int i = threadIdx.x; i < nm; i += NT) lds_dyn[i] = ms[i];
+        const float4* sp = uniform_ptr(P0->sc.spheres);
+        const int ns = uniform_int(P0->sc.sphere_num) * 2;
+        for (int i = threadIdx.x; i < ns; i += NT) lds_dyn[nm + i] = sp[i];
+        for (int i = threadIdx.x; i < S; i += NT) slot_state[i] = SLOT_FREE;
+        if (threadIdx.x == 0) walkers_done = 0;
+        __syncthreads();
+    }
+    const float4* lds_spheres = lds_dyn + uniform_int(P0->sc.material_num) * (int)(sizeof(DevMaterial) / 16);
+    float4* const q[5] = {slot_q[0], slot_q[1], slot_q[2], slot_q[3], slot_q[4]};
+    volatile int* st = slot_state;
+    int* scr = scratch[wid];
+    unsigned long long prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long segments = 0;
+    int idle = 0;
+    bool capped = false;
+    unsigned long long tc = 0;
+
+    if (wid < NWALK) {
+        // ---------------- walker wave ----------------
+        const int pbase = wid * PT_RG_PART;
+        PathState ps;
+        v3 inv = mk3(0.0f, 0.0f, 0.0f);
+        Hit h;
+        MeshWalk w;
+        int mesh = 0;
+        int ptri = -1;
+        unsigned int unit = 0;
+        int32_t pseed = 0;
+        int depth = 0;
+        int mode = LANE_WANT;
+        const unsigned int units = (unsigned int)P0->til.unit_count << batch_log2;
+        const EvenRegions regions{units, (units + PT_SHARDS - 1) / PT_SHARDS};
+        WorkCursor cursor = work_begin();
+        bool drained = false;
+        while (true) {
+            const LaunchParams* P = params;
+            asm volatile("" : "+s"(P));
+            P = uniform_ptr(P);
+            DevScene sc = load_const(&P->sc);
+            sc.materials = lds_mats;
+            sc.spheres = lds_spheres;
+            const DevConfig cfg = load_const(&P->cfg);
+            const DevTiling til = load_const(&P->til);
+            const DevOutput out = load_const(&P->out);
+            if (PROF) { prof[0]++; tc = __builtin_readcyclecounter(); }
+            const unsigned long long ready = __ballot(mode == LANE_READY);
+            const unsigned long long wantm = __ballot(mode == LANE_WANT);
+            const unsigned int nwalking = (unsigned int)__popcll(__ballot(mode == LANE_WALK || mode == LANE_TRI));
+            if ((ready | wantm) && (__popcll(ready) >= shade_min || nwalking <= (unsigned int)walk_min)) {
+                if (PROF) prof[1]++;
+                // the partition's slots: WALK ones hold paths waiting for their next segment
+                const int sv = st[pbase + lane];
+                const unsigned long long wq = __ballot(sv == SLOT_WALK), fr = __ballot(sv == SLOT_FREE);
+                if (sv == SLOT_WALK) scr[__popcll(wq & below)] = pbase + lane;
+                if (sv == SLOT_FREE) scr[64 + __popcll(fr & below)] = pbase + lane;
+                lds_fence();
+                const int nwq = __popcll(wq), nfr = __popcll(fr);
+                const int nrdy = __popcll(ready);
+                if (drained && nwalking == 0 && !ready && wantm == ~0ull && fr == ~0ull) break;
+                // ready lanes hand their path over: swap with a waiting path, else into a free slot
+                int mark = -1;
+                if (mode == LANE_READY) {
+                    const int r = __popcll(ready & below);
+                    if (r < nwq) {
+                        mark = scr[r];
+                        PathState np; unsigned int nu; int32_t nseed; int nd;
+                        slot_get(q, mark, np, nu, nseed, nd, nullptr);
+                        slot_put(q, mark, ps, unit, pseed, depth, &h);
+                        ps = np; unit = nu; pseed = nseed; depth = nd;
+                        mode = LANE_NEW;
+                    } else if (r - nwq < nfr) {
+                        mark = scr[64 + r - nwq];
+                        slot_put(q, mark, ps, unit, pseed, depth, &h);
+                        mode = LANE_WANT;
+                    }
+                }
+                if (PROF) prof[2] += (unsigned long long)__popcll(__ballot(mark >= 0));
+                lds_fence();
+                if (mark >= 0) st[mark] = SLOT_SHADE;
+                // lanes without a path take the remaining waiting paths
+                const int nswap = nrdy < nwq ? nrdy : nwq;
+                const unsigned long long want2 = __ballot(mode == LANE_WANT);
+                int pulled = -1;
+                if (mode == LANE_WANT) {
+                    const int k = nswap + __popcll(want2 & below);
+                    if (k < nwq) {
+                        pulled = scr[k];
+                        slot_get(q, pulled, ps, unit, pseed, depth, nullptr);
+                        mode = LANE_NEW;
+                    }
+                }
+                lds_fence();
+                if (pulled >= 0) st[pulled] = SLOT_FREE;
+                // and then new (pixel, pass) units (pt_work.h)
+                const bool want = mode == LANE_WANT;
+                const unsigned long long need_mask = __ballot(want);
+                if (need_mask && !drained) {
+                    const unsigned int u = work_take(out.fetch, regions.stride, regions, (unsigned int)chunk, need_mask,
+                                                     want, below, cursor, drained);
+                    if (want && u != ~0u) {
+                        unit = u;
+                        const int pixel = unit_to_pixel(til, u >> batch_log2);
+                        const int32_t hseed = hash_pt(first_pass + (int)(u & ((1u << batch_log2) - 1u)));
+                        const DevCamera cam = load_const(&P->cam);
+                        generate_path(cam, cfg, pixel, hseed, &ps);
+                        pseed = path_seed(hseed, pixel);
+                        depth = 0;
+                        if (cfg.max_depth > 0) mode = LANE_NEW;
+                        else finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
+                    }
+                }
+                if (mode == LANE_NEW) mode = begin_segment<false>(sc, lds_mesh, ps, inv, h, w, mesh);
+                if (!__any(mode == LANE_WALK || mode == LANE_TRI)) {  // waiting for the shader waves
+                    if (PROF) prof[5]++;
+                    if (++idle > PT_RG_IDLE_CAP) { capped = true; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                    if (PROF) prof[12] += __builtin_readcyclecounter() - tc;
+                    continue;
+                }
+                idle = 0;
+            }
+            if (PROF) { const unsigned long long t = __builtin_readcyclecounter(); prof[10] += t - tc; tc = t; }
+
+            const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
+            const __amdgpu_buffer_rsrc_t rt = make_rsrc(sc.tri_geom, sc.tri_count * 48);
+            auto mesh_done = [&]() {
+                if (w.tri >= 0 && w.t < h.t) {
+                    h.t = w.t; h.t1 = w.t1; h.t2 = w.t2; h.prim = w.tri; h.type = 2;
+                }
+                mesh++;
+                mode = start_mesh(sc, lds_mesh, nullptr, false, mesh, w) ? LANE_WALK : LANE_READY;
+            };
+            float4 pta = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ptb = pta, ptc = pta;
+            for (int k = 0; k < walk_steps; k++) {
+                if (k > 0 && !__any(mode == LANE_WALK || mode == LANE_TRI)) break;
+                if (PROF) { prof[3]++; prof[4] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK)); }
+                if (mode == LANE_WALK) {
+                    const bool leaf = walk_box_chain<2>(rn, ps.o, inv, w, ptri);
+                    if (leaf) {
+                        mode = LANE_TRI;
+                        pta = bload(rt, ptri * 48); ptb = bload(rt, ptri * 48 + 16); ptc = bload(rt, ptri * 48 + 32);
+                    } else if (w.pos == w.end) {
+                        mesh_done();
+                    }
+                }
+                const unsigned long long pend = __ballot(mode == LANE_TRI);
+                if (pend && (__popcll(pend) >= (unsigned int)tri_min || !__any(mode == LANE_WALK) || k == walk_steps - 1)) {
+                    if (PROF) { prof[9]++; prof[15] += (unsigned long long)__popcll(pend); }
+                    if (mode == LANE_TRI) {
+                        walk_tri_geom(pta, ptb, ptc, ps.o, ps.d, w, ptri, true);
+                        mode = LANE_WALK;
+                        if (w.pos == w.end) mesh_done();
+                    }
+                }
+            }
+            if (PROF) prof[11] += __builtin_readcyclecounter() - tc;
+        }
+        if (lane == 0) atomicAdd(&walkers_done, 1);
+    } else {
+        // ---------------- shader wave ----------------
+        const int k = wid - NWALK;
+        constexpr int NS = (S + NSHADE - 1) / NSHADE;  // slots served (k + NSHADE * j, j < NS)
+        constexpr int NC = (NS + 63) / 64;
+        const int spin_max = rg & 0xffff;
+        const int batch_min = rg >> 16;
+        int spins = 0;
+        int start = 0;  // first chunk scanned: rotates so that no partition waits behind the others
+        while (true) {
+            const LaunchParams* P = params;
+            asm volatile("" : "+s"(P));
+            P = uniform_ptr(P);
+            DevScene sc = load_const(&P->sc);
+            sc.materials = lds_mats;
+            sc.spheres = lds_spheres;
+            const DevConfig cfg = load_const(&P->cfg);
+            const DevTiling til = load_const(&P->til);
+            const DevOutput out = load_const(&P->out);
+            if (PROF) tc = __builtin_readcyclecounter();
+            unsigned long long m[NC];
+            int total = 0;
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const int j = c * 64 + lane;
+                const int s = k + NSHADE * j;
+                const int sv = (j < NS && s < S) ? st[s] : SLOT_FREE;
+                m[c] = __ballot(sv == SLOT_SHADE);
+                total += __popcll(m[c]);
+            }
+            if (total == 0 || (total < batch_min && spins < spin_max)) {
+                if (total == 0 && *(volatile int*)&walkers_done == NWALK) break;
+                spins++;
+                if (PROF) prof[8]++;
+                if (++idle > PT_RG_IDLE_CAP) { capped = true; break; }
+                __builtin_amdgcn_s_sleep(1);
+                if (PROF) prof[14] += __builtin_readcyclecounter() - tc;
+                continue;
+            }
+            spins = 0;
+            idle = 0;
+            // the first 64 waiting paths, from chunk `start` on: lane r takes the r-th
+            int base = 0;
+#pragma unroll
+            for (int cc = 0; cc < NC; cc++) {
+                const int c = (start + cc) % NC;
+                const int r = base + __popcll(m[c] & below);
+                if (((m[c] >> lane) & 1ull) && r < 64) scr[r] = k + NSHADE * (c * 64 + lane);
+                base += __popcll(m[c]);
+            }
+            start = (start + 1) % NC;
+            lds_fence();
+            const int n = total < 64 ? total : 64;
+            const bool have = lane < n;
+            int s = -1;
+            PathState ps;
+            Hit h;
+            unsigned int unit = 0;
+            int32_t pseed = 0;
+            int depth = 0;
+            bool alive = false;
+            if (have) {
+                s = scr[lane];
+                slot_get(q, s, ps, unit, pseed, depth, &h);
+                Counters none = {0u, 0u, 0u, 0u, 0u, 0u};
+                alive = shade_hit<false, FEAT>(sc, cfg, depth, pseed, &ps, h, &none);
+                depth++;
+            }
+            segments += (unsigned long long)n;
+            if (PROF) { prof[6]++; prof[7] += (unsigned long long)n; }
+            int next = SLOT_FREE;
+            if (have) {
+                if (!alive || depth >= cfg.max_depth) {
+                    finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
+                } else {
+                    slot_put(q, s, ps, unit, pseed, depth, nullptr);
+                    next = SLOT_WALK;
+                }
+            }
+            lds_fence();
+            if (have) st[s] = next;
+            if (PROF) prof[13] += __builtin_readcyclecounter() - tc;
+        }
+    }
+
+    if (lane == 0) {
+        atomicAdd(&P0->out.stats[0], segments);
+        if (capped) atomicAdd(&P0->out.stats[PT_STAT_RG_CAPPED], 1ull);  // checked by the host after the frame
+        if (PROF) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) atomicAdd(&P0->out.stats[16 + i], prof[i]);
+        }
+    }
+}
+
 // The running sum over a batch of passes, in pass order (path_tracer_kernel.cu:644-651 applied
 // pass after pass), then the 8-bit output of the batch's last pass.
 __global__ __launch_bounds__(PT_BLOCK) void accumulate_kernel(const LaunchParams* __restrict__ P, int first_pass,
@@ -775,8 +1106,53 @@ static bool use_unified(bool leaf1, bool stats, bool qn, int lds_bytes) {
     return leaf1 && !stats && unified_enabled() && lds_bytes <= PT_LDS_TABLES;
 }
 
-hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, bool wide, int feat, int first_pass,
-                       int batch_log2, int write_u8, int grid, bool stats, int lds_bytes, hipStream_t stream) {
+bool regroup_applies(bool leaf1, bool stats, bool qn, bool wide, int lds_bytes) {
+    return use_unified(leaf1, stats, qn, lds_bytes) && !qn && !wide;
+}
+
+// pass_kernel_r's wave split: PT_RG_WAVES = 10 * walkers + shaders (52: five walker waves and two
+// shader waves per workgroup of 448 lanes). MINW as pass_kernel_u: 7 without textures and media, else 6.
+struct RgKernel {
+    PassFnU fn;
+    int threads;
+};
+static RgKernel pass_fn_r(int feat) {
+    static const int split = env_int("PT_RG_WAVES", 52, 11, 99);
+    static const int prof = env_int("PT_UPROF", 0, 0, 1);
+    const bool plain = feat == 0;
+    if (prof) return {pass_kernel_r<7, 5, 2, true, 0>, 7 * 64};
+    switch (split) {
+        case 31: return {plain ? pass_kernel_r<7, 3, 1, false, 0> : pass_kernel_r<6, 3, 1, false, PT_FEAT_ALL>, 4 * 64};
+        case 61: return {plain ? pass_kernel_r<7, 6, 1, false, 0> : pass_kernel_r<6, 6, 1, false, PT_FEAT_ALL>, 7 * 64};
+        case 43: return {plain ? pass_kernel_r<7, 4, 3, false, 0> : pass_kernel_r<6, 4, 3, false, PT_FEAT_ALL>, 7 * 64};
+        case 21: return {plain ? pass_kernel_r<7, 2, 1, false, 0> : pass_kernel_r<6, 2, 1, false, PT_FEAT_ALL>, 3 * 64};
+        default: return {plain ? pass_kernel_r<7, 5, 2, false, 0> : pass_kernel_r<6, 5, 2, false, PT_FEAT_ALL>, 7 * 64};
+    }
+}
+
+hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, bool wide, int feat, bool regroup,
+                       int first_pass, int batch_log2, int write_u8, int grid, bool stats, int lds_bytes,
+                       hipStream_t stream) {
+    if (regroup && regroup_applies(leaf1, stats, qn, wide, lds_bytes)) {
+        // PT_RG_HANDOFF / PT_RG_WALK_MIN: a walker wave hands its ready paths over once this many are
+        // ready or at most this many lanes still walk; PT_RG_BATCH / PT_RG_SPIN: a shader wave shades
+        // once this many paths wait, or after this many idle rounds with fewer
+        static const int chunk = env_int("PT_CHUNK_MEGA", 64, 0, 4096);
+        static const int handoff = env_int("PT_RG_HANDOFF", 16, 1, 64);
+        static const int walk_steps = env_int("PT_WALK_STEPS", 10, 1, 64);
+        static const int tri_min = env_int("PT_TRI_MIN", 6, 1, 64);
+        static const int walk_min = env_int("PT_RG_WALK_MIN", 40, 0, 64);
+        static const int batch = env_int("PT_RG_BATCH", 48, 1, 64);
+        static const int spin = env_int("PT_RG_SPIN", 8, 0, 0xffff);
+        const RgKernel k = pass_fn_r(feat);
+        const LaunchParams* a0 = params_dev;
+        int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = handoff, a6 = walk_steps, a7 = tri_min,
+            a8 = walk_min, a9 = spin | (batch << 16);
+        void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8, &a9};
+        hipError_t e = hipLaunchKernel((const void*)k.fn, dim3(grid), dim3(k.threads), args, (size_t)lds_bytes, stream);
+        if (e != hipSuccess) return e;
+        return hipGetLastError();
+    }
     if (use_unified(leaf1, stats, qn, lds_bytes)) {
         // 64-unit chunks and a 28-lane shading batch: measured best with frames in flight
         static const int chunk = env_int("PT_CHUNK_MEGA", 64, 0, 4096);
@@ -823,9 +1199,14 @@ hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256
 }
 
 // The pass kernel launch_pass picks for these arguments, as text (bench.py's roofline.kernel).
-std::string pass_kernel_desc(bool leaf1, bool stats, bool qn, bool wide, int feat, int lds_bytes) {
+std::string pass_kernel_desc(bool leaf1, bool stats, bool qn, bool wide, int feat, bool regroup, int lds_bytes) {
     char buf[160];
-    if (use_unified(leaf1, stats, qn, lds_bytes)) {
+    if (regroup && regroup_applies(leaf1, stats, qn, wide, lds_bytes)) {
+        static const int split = env_int("PT_RG_WAVES", 52, 11, 99);
+        const int s = (split == 31 || split == 61 || split == 43 || split == 21) ? split : 52;
+        std::snprintf(buf, sizeof(buf), "pass_kernel_r<MINW=%d,NWALK=%d,NSHADE=%d,FEAT=%d>", feat == 0 ? 7 : 6, s / 10,
+                      s % 10, feat == 0 ? 0 : PT_FEAT_ALL);
+    } else if (use_unified(leaf1, stats, qn, lds_bytes)) {
         static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
         static const int chain = env_int("PT_WALK_CHAIN", 2, 1, 3);
         static const int pf = env_int("PT_TRI_PREFETCH", 1, 0, 1);
@@ -839,10 +1220,18 @@ std::string pass_kernel_desc(bool leaf1, bool stats, bool qn, bool wide, int fea
     return buf;
 }
 
-int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int feat, int lds_bytes) {
+int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int feat, bool regroup, int lds_bytes) {
     int dev = 0, cus = 0, blocks = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+    if (regroup && regroup_applies(leaf1, stats, qn, wide, lds_bytes)) {
+        const RgKernel k = pass_fn_r(feat);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, (const void*)k.fn, k.threads, (size_t)lds_bytes) !=
+                hipSuccess || blocks <= 0)
+            blocks = 1;
+        return cus * blocks;
+    }
     const bool u = use_unified(leaf1, stats, qn, lds_bytes);
     const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true, feat), qn, wide && !qn, feat)
                        : (const void*)pass_fn(leaf1, stats, pass_min_waves(false, feat), qn);

@@ -468,7 +468,8 @@ struct pt_context {
     bool instrumented = false;
     int schedule = -1;  // PT_SCHEDULE_*; -1: environment default (PT_MODE)
     int wide_mode = -1; // pass_kernel_u walks the wide records: 1 on, 0 off, -1 environment default (PT_WIDE)
-    int grid[2][2][3][4] = {};
+    int regroup_mode = -1;  // pass_kernel_r (walker and shader waves): 1 on, 0 off, -1 environment default (PT_REGROUP)
+    int grid[2][2][4][4] = {};
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
     size_t ev_used = 0;
@@ -675,6 +676,16 @@ bool use_wide(const pt_context* ctx) {
     return want && ctx->scene.wide != nullptr && !ctx->refitted && !use_qnodes(ctx);
 }
 
+// PT_REGROUP=1 runs pass_kernel_r (pt_kernels.hip: walker waves and shader waves regrouping paths
+// through LDS) where pass_kernel_u would run.
+bool use_regroup(const pt_context* ctx) {
+    static int on = [] {
+        const char* e = getenv("PT_REGROUP");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return ctx->regroup_mode >= 0 ? ctx->regroup_mode != 0 : on;
+}
+
 // dynamic LDS of pass_kernel_u: every material, then every sphere record (pt_kernels.hip)
 int pass_lds_bytes(const pt_context* ctx) {
     return ctx->material_num * (int)sizeof(DevMaterial) + ctx->scene.sphere_num * 32;
@@ -690,10 +701,10 @@ int render_feat(const pt_context* ctx, const DevConfig& dc) {
 }
 
 int pass_grid(pt_context* ctx, int feat) {
-    const bool leaf1 = ctx->scene.leaf_size == 1, qn = use_qnodes(ctx), wide = use_wide(ctx);
-    int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0][qn ? 1 : (wide ? 2 : 0)][feat & 3];
+    const bool leaf1 = ctx->scene.leaf_size == 1, qn = use_qnodes(ctx), wide = use_wide(ctx), rg = use_regroup(ctx);
+    int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0][qn ? 1 : (wide ? 2 : (rg ? 3 : 0))][feat & 3];
     if (g == 0) {
-        g = pass_grid_size(leaf1, ctx->instrumented, qn, wide, feat, pass_lds_bytes(ctx));
+        g = pass_grid_size(leaf1, ctx->instrumented, qn, wide, feat, rg, pass_lds_bytes(ctx));
         // PT_GRID_PCT: experiment knob, a percentage of the occupancy-sized grid
         const char* e = getenv("PT_GRID_PCT");
         const int pct = e ? atoi(e) : 100;
@@ -841,7 +852,7 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     const int feat = render_feat(ctx, dc);
     const int grid = pass_grid(ctx, feat);
     ctx->last_kernel = pass_kernel_desc(ctx->scene.leaf_size == 1, ctx->instrumented, use_qnodes(ctx), use_wide(ctx),
-                                        feat, pass_lds_bytes(ctx));
+                                        feat, use_regroup(ctx), pass_lds_bytes(ctx));
     const int units = ctx->tiling.unit_count;
     int most = 1;
     while (most * 2 <= max_pass_batch() && (long long)units * most * 2 <= (1ll << 28)) most *= 2;
@@ -866,7 +877,8 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
         int rc = ev_begin(ctx, 0);
         if (rc != PT_OK) return rc;
-        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, use_qnodes(ctx), use_wide(ctx), feat, first, lg, w8, grid,
+        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, use_qnodes(ctx), use_wide(ctx), feat, use_regroup(ctx),
+                           first, lg, w8, grid,
                            ctx->instrumented, pass_lds_bytes(ctx), ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         if (lg > 0) {
@@ -996,6 +1008,12 @@ extern "C" int pt_scene_info(pt_context* ctx, long long* bytes, int* node_num, i
 extern "C" int pt_set_wide_walk(pt_context* ctx, int mode) {
     if (!ctx || mode < -1 || mode > 1) { set_error("bad wide walk mode"); return PT_E_ARG; }
     ctx->wide_mode = mode;
+    return PT_OK;
+}
+
+extern "C" int pt_set_regroup(pt_context* ctx, int mode) {
+    if (!ctx || mode < -1 || mode > 1) { set_error("bad regroup mode"); return PT_E_ARG; }
+    ctx->regroup_mode = mode;
     return PT_OK;
 }
 

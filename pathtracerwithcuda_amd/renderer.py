@@ -89,6 +89,11 @@ class Renderer:
         """True: walk the wide BVH records when the scene has them; False: the binary nodes; None: PT_WIDE."""
         check(self._lib.pt_set_wide_walk(self._ctx, -1 if on is None else int(bool(on))), "pt_set_wide_walk")
 
+    def set_regroup(self, on: bool | None) -> None:
+        """True: walker and shader waves regroup paths through LDS (pass_kernel_r); False: every wave walks
+        and shades (pass_kernel_u); None: PT_REGROUP. The image is the same either way."""
+        check(self._lib.pt_set_regroup(self._ctx, -1 if on is None else int(bool(on))), "pt_set_regroup")
+
     def attach_mesh(self, scene: Scene, mesh: int) -> None:
         """Keep mesh `mesh`'s local triangles and initial boxes on the device for set_mesh_transform."""
         d = scene.mesh_local(mesh)
@@ -144,6 +149,13 @@ class Renderer:
         check(self._lib.pt_stats_all(self._ctx, a, 7), "pt_stats_all")
         keys = ("segments", "nodes", "tris", "hit_mesh", "hit_sphere", "miss", "scatter")
         return dict(zip(keys, (int(x) for x in a)))
+
+    def stats_raw(self, n: int = 32) -> list[int]:
+        """The context's raw statistics words (stats[15]: pass_kernel_r waves that gave up waiting, always 0;
+        stats[16..]: PT_UPROF counters)."""
+        a = (C.c_ulonglong * n)()
+        check(self._lib.pt_stats_all(self._ctx, a, n), "pt_stats_all")
+        return [int(x) for x in a]
 
     SCHEDULES = {"persistent": 0, "wavefront": 1}
 

@@ -35,17 +35,20 @@ def assert_bitwise(gpu, ref, what=""):
                              f"max |d| {np.nanmax(d):.3g}, mean |d| {np.nanmean(d):.3g}")
 
 
-@pytest.fixture(scope="module", params=["persistent", "persistent_wide", "wavefront"])
+@pytest.fixture(scope="module", params=["persistent", "persistent_wide", "persistent_regroup", "wavefront"])
 def gpu(require_gpu, request):
     """Every parity test runs under both kernel schedules (pt_set_schedule), and the persistent one both
     with its default walk (the binary nodes) and walking the wide BVH records where the scene has them
-    (pt_set_wide_walk, pt_path.h walk_wide): they must all agree bitwise."""
+    (pt_set_wide_walk, pt_path.h walk_wide) and as walker and shader waves (pt_set_regroup,
+    pass_kernel_r): they must all agree bitwise."""
     r = pt.Renderer(0)
     sched = "wavefront" if request.param == "wavefront" else "persistent"
     r.set_schedule(sched)
     assert r.schedule() == sched
     if request.param == "persistent_wide":
         r.set_wide_walk(True)
+    if request.param == "persistent_regroup":
+        r.set_regroup(True)
     yield r
     r.close()
 
@@ -317,6 +320,37 @@ def test_c5_4k_textured_depth12_frame(bench_gpu):
     assert wl.depth == 12 and (wl.width, wl.height) == (3840, 2160)
     launches, _ = _render_workload_subset(bench_gpu, wl, passes=8)
     assert launches == {0: 1, 3: 1}, launches
+
+
+@pytest.mark.parametrize("workload", ["metric", "c4", "c5"])
+def test_regrouped_waves_at_the_bench_launch_shape(bench_gpu, c4_workload, workload):
+    """pass_kernel_r (walker waves and shader waves exchanging paths through LDS) on the bench's launch
+    shape and the C4/C5 configurations: bit-identical to the oracle on a pixel subset and to pass_kernel_u
+    on the whole frame, the same ray-segment count, and no wave gave up waiting (stats[15])."""
+    import bench
+    wl = c4_workload if workload == "c4" else bench.Workload(workload)
+    r = bench_gpu
+    r.upload(wl.scene, wl.cfg)
+    r.setup_frame(wl.width, wl.height)
+    r.stats_reset()
+    r.render(wl.cam, wl.cfg, 1, 8, write_u8=2)
+    r.synchronize()
+    base, base8 = r.download()
+    base_segments = r.stats()["segments"]
+    assert r.last_kernel().startswith("pass_kernel_u")
+    r.set_regroup(True)
+    try:
+        launches, img = _render_workload_subset(r, wl, passes=8, npx=10000, seed=3)
+        assert r.last_kernel().startswith("pass_kernel_r"), r.last_kernel()
+        raw = r.stats_raw()
+        assert raw[15] == 0, "a pass_kernel_r wave gave up waiting"
+        assert raw[0] == base_segments
+        assert launches == {0: 1, 3: 1}, launches
+        img8 = r.download()[1]
+    finally:
+        r.set_regroup(None)
+    assert np.array_equal(img, base)
+    assert np.array_equal(img8, base8)
 
 
 @pytest.mark.parametrize("bands", [4, 8])
