@@ -6,9 +6,9 @@ A step is one frame: 8 passes (batched into one persistent HIP launch plus an in
 over the 1920x1080 frame and the 8-bit gamma output; with N > 1 each rank renders its interleaved 8-row bands and
 rank 0 gathers the ranks' rows of the float accumulation buffer with one RCCL gather (torch.distributed
 "nccl"; PT_FRAME_COLLECTIVE=reduce: one reduce of the whole buffer instead), after which rank 0
-writes the 8-bit image. Frames are queued with no host synchronisation on two (three when N >= 4)
-renderer contexts, so one frame's tail overlaps the next frame's start (PT_BENCH_INFLIGHT=1: one at
-a time); the host-synchronised single-frame latency is reported beside it. Mrays/s = ray segments traced (the live-ray counts the
+writes the 8-bit image. Frames are queued with no host synchronisation on three renderer contexts,
+each launching on half the grid, so one frame's tail overlaps the next frames' work (PT_BENCH_INFLIGHT=1:
+one at a time on the whole grid); the host-synchronised single-frame latency is reported beside it. Mrays/s = ray segments traced (the live-ray counts the
 reference's thread_shrink returns, summed over passes and depths and over ranks) / wall time.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -221,7 +221,11 @@ def main() -> int:
             dist.init_process_group(backend)
     # frames in flight: one renderer context (own stream, image and pass buffers) per frame in flight,
     # so the next frame's workgroups fill the previous frame's tail; 1 = one at a time
-    inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or (2 if world <= 2 else 3)
+    inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or 3
+    # with three frames in flight each launch takes half the occupancy-sized grid (pt_set_grid_share):
+    # 6.35 vs 6.58 ms/frame at N = 1 (two in flight, whole grid), 1.10 vs 1.36 ms for an 8-way share
+    # (profiles/r02/scaling/grid_share.txt)
+    grid_share = int(os.environ.get("PT_BENCH_GRID_SHARE", "50")) if inflight >= 3 else 100
     wl = Workload(args.workload)
     scene, cfg, cam = wl.scene, wl.cfg, wl.cam
     width, height, spp = wl.width, wl.height, wl.spp
@@ -229,6 +233,7 @@ def main() -> int:
     for _ in range(inflight):
         q = pt.Renderer(local)
         q.set_schedule(args.schedule)
+        q.set_grid_share(grid_share)
         q.upload(scene, cfg)
         rs.append(q)
         frames.append(pt.TiledFrame(q, width, height, dist if world > 1 else None, BAND_ROWS,
@@ -274,6 +279,7 @@ def main() -> int:
     # dominant kernel's launch duration for the roofline is taken here too, with no other frame in flight
     # (with frames in flight the HIP events of one launch also span the overlapping launch's work)
     lat_frames = max(3, min(5, args.steps))
+    r.set_grid_share(100)
     r.stats_reset()
     if world > 1:
         dist.barrier()
@@ -359,6 +365,7 @@ def main() -> int:
             "band_rows": BAND_ROWS if world > 1 else None,
             "ms_per_frame": round(ms_per_step, 3),
             "frames_in_flight": inflight,
+            "grid_share_pct": grid_share,
             "ms_per_frame_latency": round(latency * 1000.0, 3),
             "camera_samples_per_s_M": round(width * height * spp * args.steps / elapsed / 1e6, 3),
             "segments_per_frame": segments // max(args.steps, 1),

@@ -46,6 +46,10 @@ int pt_set_wide_walk(pt_context* ctx, int mode);
 /* 1: run the pass as walker waves and shader waves that regroup paths through LDS (pass_kernel_r),
  * 0: every wave walks and shades (pass_kernel_u), -1: PT_REGROUP (default 0). Same results either way. */
 int pt_set_regroup(pt_context* ctx, int mode);
+/* The percentage (1-100, default 100) of the occupancy-sized grid this context's pass launches take:
+ * with several contexts rendering frames in flight, the rest of the CUs run the other frames
+ * (DESIGN.md §6). Results do not depend on it. */
+int pt_set_grid_share(pt_context* ctx, int percent);
 /* The pass kernel (and its template configuration) the last render call of this context launched. */
 const char* pt_last_kernel(pt_context* ctx);
 

@@ -192,6 +192,7 @@ _PROTOS = {
     "pt_scene_walk_info": (C.c_int, [C.c_void_p, c_int_p, c_int_p]),
     "pt_set_wide_walk": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_regroup": (C.c_int, [C.c_void_p, C.c_int]),
+    "pt_set_grid_share": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_last_kernel": (C.c_char_p, [C.c_void_p]),
     "pt_mesh_attach": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Triangle), C.c_int, C.c_int, C.POINTER(BoundingBox),
                                  C.c_int, Float3, Float3]),

@@ -468,7 +468,8 @@ struct pt_context {
     bool instrumented = false;
     int schedule = -1;  // PT_SCHEDULE_*; -1: environment default (PT_MODE)
     int wide_mode = -1; // pass_kernel_u walks the wide records: 1 on, 0 off, -1 environment default (PT_WIDE)
-    int regroup_mode = -1;  // pass_kernel_r (walker and shader waves): 1 on, 0 off, -1 environment default (PT_REGROUP)
+    int regroup_mode = -1;
+    int grid_share = 100;  // pt_set_grid_share: percent of the occupancy-sized grid a pass launch takes  // pass_kernel_r (walker and shader waves): 1 on, 0 off, -1 environment default (PT_REGROUP)
     int grid[2][2][4][4] = {};
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
@@ -713,6 +714,14 @@ int pass_grid(pt_context* ctx, int feat) {
     return g;
 }
 
+// With several frames in flight each launch may take a share of the occupancy-sized grid: the slots it
+// leaves run the other frames' launches, so no frame's tail leaves CUs idle (bench.py: three frames in
+// flight at 50 %, DESIGN.md §6, profiles/r02/scaling).
+int shared_grid(const pt_context* ctx, int grid) {
+    if (ctx->grid_share >= 100) return grid;
+    return std::max(8, (int)((long long)grid * ctx->grid_share / 100));
+}
+
 int ev_begin(pt_context* ctx, int kind) {
     if (ctx->ev_used == ctx->ev_start.size()) {
         hipEvent_t a, b;
@@ -873,12 +882,13 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         while (b * 2 <= most && i + b * 2 <= pass_count) { b *= 2; lg++; }
         const int first = first_pass + i;
         const int last = i + b == pass_count;
+        const int g = shared_grid(ctx, grid);
         const int w8 = write_u8 == 1 || (write_u8 == 2 && last);
         PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
         int rc = ev_begin(ctx, 0);
         if (rc != PT_OK) return rc;
         PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, use_qnodes(ctx), use_wide(ctx), feat, use_regroup(ctx),
-                           first, lg, w8, grid,
+                           first, lg, w8, g,
                            ctx->instrumented, pass_lds_bytes(ctx), ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         if (lg > 0) {
@@ -1008,6 +1018,12 @@ extern "C" int pt_scene_info(pt_context* ctx, long long* bytes, int* node_num, i
 extern "C" int pt_set_wide_walk(pt_context* ctx, int mode) {
     if (!ctx || mode < -1 || mode > 1) { set_error("bad wide walk mode"); return PT_E_ARG; }
     ctx->wide_mode = mode;
+    return PT_OK;
+}
+
+extern "C" int pt_set_grid_share(pt_context* ctx, int percent) {
+    if (!ctx || percent < 1 || percent > 100) { set_error("bad grid share"); return PT_E_ARG; }
+    ctx->grid_share = percent;
     return PT_OK;
 }
 

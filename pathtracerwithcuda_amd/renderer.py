@@ -94,6 +94,10 @@ class Renderer:
         and shades (pass_kernel_u); None: PT_REGROUP. The image is the same either way."""
         check(self._lib.pt_set_regroup(self._ctx, -1 if on is None else int(bool(on))), "pt_set_regroup")
 
+    def set_grid_share(self, percent: int) -> None:
+        """Percentage of the occupancy-sized grid this context's pass launches take (frames in flight)."""
+        check(self._lib.pt_set_grid_share(self._ctx, int(percent)), "pt_set_grid_share")
+
     def attach_mesh(self, scene: Scene, mesh: int) -> None:
         """Keep mesh `mesh`'s local triangles and initial boxes on the device for set_mesh_transform."""
         d = scene.mesh_local(mesh)

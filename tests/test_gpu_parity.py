@@ -353,6 +353,29 @@ def test_regrouped_waves_at_the_bench_launch_shape(bench_gpu, c4_workload, workl
     assert np.array_equal(img8, base8)
 
 
+def test_grid_share_changes_nothing_but_the_grid(bench_gpu):
+    """pt_set_grid_share (half the grid per launch, bench.py with three frames in flight): rank 0's
+    share of an 8-way tiled metric frame is the same image bit for bit."""
+    import bench
+    wl = bench.Workload("metric")
+    r = bench_gpu
+    r.upload(wl.scene, wl.cfg)
+    r.setup_frame(wl.width, wl.height)
+    r.set_tiling(bench.BAND_ROWS, 8, 0)
+    try:
+        r.render(wl.cam, wl.cfg, 1, 8, write_u8=2)
+        full, full8 = r.download()
+        r.render(wl.cam, wl.cfg, 1, 1, write_u8=2)  # overwrite the share with a different frame
+        assert not np.array_equal(r.download()[0], full)
+        r.set_grid_share(50)
+        r.render(wl.cam, wl.cfg, 1, 8, write_u8=2)
+        img, img8 = r.download()
+    finally:
+        r.set_grid_share(100)
+        r.set_tiling(bench.BAND_ROWS, 1, 0)
+    assert np.array_equal(img, full) and np.array_equal(img8, full8)
+
+
 @pytest.mark.parametrize("bands", [4, 8])
 def test_c4_band_tiling_partitions_the_frame(bench_gpu, c4_workload, bands):
     """The multi-GPU partition on the C4 scene at the bench's 8-row bands: every rank's share rendered

@@ -25,11 +25,13 @@ def main() -> None:
     ap.add_argument("--counts", default="1,2,4,8")
     ap.add_argument("--inflight", type=int, default=1, help="frames in flight (one renderer context each)")
     ap.add_argument("--ranks-max", type=int, default=8, help="time at most this many ranks per N")
+    ap.add_argument("--share", type=int, default=100, help="pt_set_grid_share: percent of the grid per launch")
     args = ap.parse_args()
     wl = bench.Workload("metric")
     rs = []
     for _ in range(args.inflight):
         r = pt.Renderer(0)
+        r.set_grid_share(args.share)
         r.upload(wl.scene, wl.cfg)
         r.setup_frame(wl.width, wl.height)
         rs.append(r)
