@@ -50,6 +50,16 @@ int pt_set_regroup(pt_context* ctx, int mode);
  * with several contexts rendering frames in flight, the rest of the CUs run the other frames
  * (DESIGN.md §6). Results do not depend on it. */
 int pt_set_grid_share(pt_context* ctx, int percent);
+/* Band order of the work queue. The context's pixels are bands of band_rows rows
+ * (pt_set_tiling; one context: bands of the whole frame). pt_band_count gives their number and whether
+ * the last is partial; pt_set_band_order(order, n) hands out local band order[i] i-th (a permutation
+ * that keeps a partial last band last; n = 0 restores the row order); pt_band_cost_enable(1) zeroes
+ * and starts per-band ray-segment counters, which pt_band_cost downloads after the context's work.
+ * Orders and counters belong to the current tiling and frame size. Results do not depend on them. */
+int pt_band_count(pt_context* ctx, int* bands, int* last_partial);
+int pt_set_band_order(pt_context* ctx, const int* order, int n);
+int pt_band_cost_enable(pt_context* ctx, int on);
+int pt_band_cost(pt_context* ctx, unsigned int* out, int n);
 /* The pass kernel (and its template configuration) the last render call of this context launched. */
 const char* pt_last_kernel(pt_context* ctx);
 

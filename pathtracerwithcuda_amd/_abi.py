@@ -193,6 +193,10 @@ _PROTOS = {
     "pt_set_wide_walk": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_regroup": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_grid_share": (C.c_int, [C.c_void_p, C.c_int]),
+    "pt_band_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "pt_set_band_order": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.c_int]),
+    "pt_band_cost_enable": (C.c_int, [C.c_void_p, C.c_int]),
+    "pt_band_cost": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint), C.c_int]),
     "pt_last_kernel": (C.c_char_p, [C.c_void_p]),
     "pt_mesh_attach": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Triangle), C.c_int, C.c_int, C.POINTER(BoundingBox),
                                  C.c_int, Float3, Float3]),

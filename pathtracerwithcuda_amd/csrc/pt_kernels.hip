@@ -241,9 +241,11 @@ __device__ __forceinline__ int begin_segment(const DevScene& sc, const int2* lds
 }
 
 // pixel_256_transform_gamma_corrected_kernel (:644-680) for one finished (pixel, pass) unit
+// depth: the path's ray segments, counted into its band when the context measures band costs.
 __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfig& cfg, const DevOutput& out,
                                             const PathState& ps, unsigned int unit, int first_pass, int write_u8,
-                                            int batch_log2, float clamp_hi) {
+                                            int batch_log2, float clamp_hi, int depth) {
+    if (til.band_cost) atomicAdd(&til.band_cost[pixel_band(til, unit_to_pixel(til, unit >> batch_log2))], (unsigned int)depth);
     const v3 c = clamp3(ps.rad, 0.0f, clamp_hi);
     if (batch_log2 == 0) {
         const int pixel = unit_to_pixel(til, unit);
@@ -348,7 +350,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     if (cfg.max_depth > 0) {
                         mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
                     } else {
-                        finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
+                        finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
                     }
                 } else if (drained) {
                     mode = LANE_DONE;
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (mode == LANE_READY) {  // the pass's end for this unit, or the next trace step
                 depth++;
                 if (!alive || depth >= cfg.max_depth) {
-                    finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
+                    finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
                     mode = LANE_WANT;
                 } else {
                     mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
@@ -660,7 +662,7 @@ __global__ __launch_bounds__((NWALK + NSHADE) * 64, MINW) void pass_kernel_r(
                         pseed = path_seed(hseed, pixel);
                         depth = 0;
                         if (cfg.max_depth > 0) mode = LANE_NEW;
-                        else finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
+                        else finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
                     }
                 }
                 if (mode == LANE_NEW) mode = begin_segment<false>(sc, lds_mesh, ps, inv, h, w, mesh);
@@ -783,7 +785,7 @@ __global__ __launch_bounds__((NWALK + NSHADE) * 64, MINW) void pass_kernel_r(
             int next = SLOT_FREE;
             if (have) {
                 if (!alive || depth >= cfg.max_depth) {
-                    finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi);
+                    finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
                 } else {
                     slot_put(q, s, ps, unit, pseed, depth, nullptr);
                     next = SLOT_WALK;

@@ -460,7 +460,7 @@ struct pt_context {
     uint8_t* image256 = nullptr;   // uchar3
     bool own_image = false;
     size_t image_cap = 0, image256_cap = 0;
-    DevTiling tiling{0, 0, 1, 1, 0, 0};
+    DevTiling tiling{0, 0, 1, 1, 0, 0, nullptr, nullptr};
     // counters
     unsigned int* fetch = nullptr;
     unsigned long long* stats = nullptr;
@@ -468,8 +468,16 @@ struct pt_context {
     bool instrumented = false;
     int schedule = -1;  // PT_SCHEDULE_*; -1: environment default (PT_MODE)
     int wide_mode = -1; // pass_kernel_u walks the wide records: 1 on, 0 off, -1 environment default (PT_WIDE)
-    int regroup_mode = -1;
-    int grid_share = 100;  // pt_set_grid_share: percent of the occupancy-sized grid a pass launch takes  // pass_kernel_r (walker and shader waves): 1 on, 0 off, -1 environment default (PT_REGROUP)
+    int regroup_mode = -1;  // pass_kernel_r (walker and shader waves): 1 on, 0 off, -1 environment default (PT_REGROUP)
+    int grid_share = 100;   // pt_set_grid_share: percent of the occupancy-sized grid a pass launch takes
+    // pt_set_band_order / pt_band_cost: the order in which this context's bands are handed out, and
+    // per-band ray-segment counters (allocated while measuring); both for the current tiling only
+    int* band_order = nullptr;
+    int band_order_n = 0;
+    int band_order_h = 0;  // frame height the order was set for
+    unsigned int* band_cost = nullptr;
+    int band_cost_n = 0;
+    bool band_cost_on = false;
     int grid[2][2][4][4] = {};
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
@@ -654,6 +662,31 @@ void update_tiling(pt_context* ctx) {
     t.unit_count = rows * ctx->width;
 }
 
+// This context's bands under its tiling, in unit order, and whether the last one is partial (fewer
+// than band_rows rows: it stays last in any band order, pt_work.h unit_to_pixel).
+int local_bands(const pt_context* ctx, bool* last_partial) {
+    const DevTiling& t = ctx->tiling;
+    const int count = t.band_count > 1 ? t.band_count : 1, index = t.band_count > 1 ? t.band_index : 0;
+    int n = 0;
+    bool partial = false;
+    for (int b = index; b * t.band_rows < ctx->height; b += count) {
+        n++;
+        partial = (b + 1) * t.band_rows > ctx->height;
+    }
+    if (last_partial) *last_partial = partial;
+    return n;
+}
+
+void clear_band_order(pt_context* ctx) {
+    if (ctx->band_order) (void)hipFree(ctx->band_order);
+    if (ctx->band_cost) (void)hipFree(ctx->band_cost);
+    ctx->band_order = nullptr;
+    ctx->band_order_n = 0;
+    ctx->band_cost = nullptr;
+    ctx->band_cost_n = 0;
+    ctx->band_cost_on = false;
+}
+
 // PT_QNODES=1 walks the 16-B quantised nodes (bit-identical; measured slower than the exact
 // 32-B walk on MI355X at 1080p, DESIGN.md §3.1, so off by default).
 bool use_qnodes(const pt_context* ctx) {
@@ -823,6 +856,11 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     lp.cfg = dc;
     lp.cam = dcam;
     lp.til = ctx->tiling;
+    const int nb = (ctx->band_order || ctx->band_cost_on) ? local_bands(ctx, nullptr) : 0;
+    // an order is used only for the frame height and tiling it was set for (set_tiling drops it)
+    lp.til.band_order = ctx->band_order && ctx->band_order_n == nb && ctx->band_order_h == ctx->height ? ctx->band_order
+                                                                                                       : nullptr;
+    lp.til.band_cost = ctx->band_cost_on && ctx->band_cost_n == nb ? ctx->band_cost : nullptr;
     lp.out = out;
     const int D = dc.max_depth > 0 ? dc.max_depth : 0;
     if (!ctx->mat_air_n_valid || ctx->mat_air_n != dc.air_n) {  // DevMaterial shading constants
@@ -971,6 +1009,7 @@ extern "C" void pt_context_destroy(pt_context* ctx) {
     if (ctx->params) (void)hipFree(ctx->params);
     if (ctx->wave_mem) (void)hipFree(ctx->wave_mem);
     if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
+    clear_band_order(ctx);
     if (ctx->shrink_buf) (void)hipFree(ctx->shrink_buf);
     if (ctx->shrink_tiles) (void)hipFree(ctx->shrink_tiles);
     if (ctx->shrink_total) (void)hipFree(ctx->shrink_total);
@@ -1117,9 +1156,86 @@ extern "C" int pt_set_tiling(pt_context* ctx, int band_rows, int band_count, int
         set_error("bad tiling");
         return PT_E_ARG;
     }
+    if (ctx->tiling.band_rows != band_rows || ctx->tiling.band_count != band_count ||
+        ctx->tiling.band_index != band_index) {
+        if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+        clear_band_order(ctx);  // the bands changed
+    }
     ctx->tiling.band_rows = band_rows;
     ctx->tiling.band_count = band_count;
     ctx->tiling.band_index = band_index;
+    return PT_OK;
+}
+
+extern "C" int pt_band_count(pt_context* ctx, int* bands, int* last_partial) {
+    if (!ctx) return PT_E_ARG;
+    if (!ctx->width) { set_error("no frame set up"); return PT_E_STATE; }
+    bool partial = false;
+    const int n = local_bands(ctx, &partial);
+    if (bands) *bands = n;
+    if (last_partial) *last_partial = partial ? 1 : 0;
+    return PT_OK;
+}
+
+extern "C" int pt_set_band_order(pt_context* ctx, const int* order, int n) {
+    if (!ctx) return PT_E_ARG;
+    if (n == 0 || !order) {
+        if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+        if (ctx->band_order) (void)hipFree(ctx->band_order);
+        ctx->band_order = nullptr;
+        ctx->band_order_n = 0;
+        return PT_OK;
+    }
+    if (!ctx->width) { set_error("no frame set up"); return PT_E_STATE; }
+    bool partial = false;
+    const int nb = local_bands(ctx, &partial);
+    if (n != nb) { set_error("band order: wrong band count for this tiling"); return PT_E_ARG; }
+    std::vector<char> seen((size_t)n, 0);
+    for (int i = 0; i < n; i++) {
+        if (order[i] < 0 || order[i] >= n || seen[(size_t)order[i]]) { set_error("band order: not a permutation"); return PT_E_ARG; }
+        seen[(size_t)order[i]] = 1;
+    }
+    if (partial && order[n - 1] != n - 1) { set_error("band order: the partial last band must stay last"); return PT_E_ARG; }
+    int rc = ensure_device(ctx);
+    if (rc != PT_OK) return rc;
+    if (ctx->stream) PT_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->band_order_n != n) {
+        if (ctx->band_order) (void)hipFree(ctx->band_order);
+        ctx->band_order = nullptr;
+        ctx->band_order_n = 0;
+        PT_HIP(hipMalloc(&ctx->band_order, (size_t)n * sizeof(int)));
+        ctx->band_order_n = n;
+    }
+    PT_HIP(hipMemcpy(ctx->band_order, order, (size_t)n * sizeof(int), hipMemcpyHostToDevice));
+    ctx->band_order_h = ctx->height;
+    return PT_OK;
+}
+
+extern "C" int pt_band_cost_enable(pt_context* ctx, int on) {
+    if (!ctx) return PT_E_ARG;
+    if (!on) { ctx->band_cost_on = false; return PT_OK; }
+    if (!ctx->width) { set_error("no frame set up"); return PT_E_STATE; }
+    int rc = ensure_device(ctx);
+    if (rc != PT_OK) return rc;
+    const int n = local_bands(ctx, nullptr);
+    if (ctx->stream) PT_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->band_cost_n != n) {
+        if (ctx->band_cost) (void)hipFree(ctx->band_cost);
+        ctx->band_cost = nullptr;
+        ctx->band_cost_n = 0;
+        PT_HIP(hipMalloc(&ctx->band_cost, (size_t)n * sizeof(unsigned int)));
+        ctx->band_cost_n = n;
+    }
+    PT_HIP(hipMemset(ctx->band_cost, 0, (size_t)n * sizeof(unsigned int)));
+    ctx->band_cost_on = true;
+    return PT_OK;
+}
+
+extern "C" int pt_band_cost(pt_context* ctx, unsigned int* out, int n) {
+    if (!ctx || !out) return PT_E_ARG;
+    if (!ctx->band_cost || n != ctx->band_cost_n) { set_error("band cost: not measured for this tiling"); return PT_E_STATE; }
+    PT_HIP(hipStreamSynchronize(ctx->stream));
+    PT_HIP(hipMemcpy(out, ctx->band_cost, (size_t)n * sizeof(unsigned int), hipMemcpyDeviceToHost));
     return PT_OK;
 }
 

@@ -128,6 +128,11 @@ struct DevTiling {
     int band_count;
     int band_index;
     int unit_count;  // pixels owned
+    // optional: band_order[i] = the local band the i-th band of units covers (a permutation that keeps
+    // a partial last band last; pt_set_band_order), band_cost[b] += ray segments of local band b's
+    // finished paths (pt_band_cost_enable). Neither changes a result.
+    const int* band_order;
+    unsigned int* band_cost;
 };
 
 struct DevOutput {

@@ -98,6 +98,45 @@ class Renderer:
         """Percentage of the occupancy-sized grid this context's pass launches take (frames in flight)."""
         check(self._lib.pt_set_grid_share(self._ctx, int(percent)), "pt_set_grid_share")
 
+    def band_count(self) -> tuple[int, bool]:
+        """(bands of this context's share under its tiling, whether the last one is partial)."""
+        n, p = C.c_int(), C.c_int()
+        check(self._lib.pt_band_count(self._ctx, C.byref(n), C.byref(p)), "pt_band_count")
+        return n.value, bool(p.value)
+
+    def set_band_order(self, order) -> None:
+        """Hand out local band order[i] i-th (None: row order). Results do not depend on it."""
+        if order is None:
+            check(self._lib.pt_set_band_order(self._ctx, None, 0), "pt_set_band_order")
+            return
+        a = (C.c_int * len(order))(*[int(x) for x in order])
+        check(self._lib.pt_set_band_order(self._ctx, a, len(order)), "pt_set_band_order")
+
+    def measure_band_cost(self, on: bool) -> None:
+        """Zero and start (True) or stop (False) the per-band ray-segment counters."""
+        check(self._lib.pt_band_cost_enable(self._ctx, int(bool(on))), "pt_band_cost_enable")
+
+    def band_cost(self) -> list[int]:
+        """Ray segments per local band since measure_band_cost(True) (waits for the context's work)."""
+        n, _ = self.band_count()
+        a = (C.c_uint * n)()
+        check(self._lib.pt_band_cost(self._ctx, a, n), "pt_band_cost")
+        return [int(x) for x in a]
+
+    def order_bands_by_cost(self, cam: RenderCamera, config: Configuration, passes: int) -> list[int]:
+        """Render one (untimed) frame measuring each band's ray segments, then hand the bands out most
+        expensive first (a partial last band stays last). Returns the order."""
+        self.set_band_order(None)
+        self.measure_band_cost(True)
+        self.render(cam, config, 1, passes, write_u8=0)
+        cost = self.band_cost()
+        self.measure_band_cost(False)
+        n, partial = self.band_count()
+        full = n - 1 if partial else n
+        order = sorted(range(full), key=lambda b: (-cost[b], b)) + ([n - 1] if partial else [])
+        self.set_band_order(order)
+        return order
+
     def attach_mesh(self, scene: Scene, mesh: int) -> None:
         """Keep mesh `mesh`'s local triangles and initial boxes on the device for set_mesh_transform."""
         d = scene.mesh_local(mesh)

@@ -376,6 +376,49 @@ def test_grid_share_changes_nothing_but_the_grid(bench_gpu):
     assert np.array_equal(img, full) and np.array_equal(img8, full8)
 
 
+@pytest.mark.parametrize("share", [1, 8])
+def test_band_order_changes_nothing_but_the_order(bench_gpu, share):
+    """pt_set_band_order (bands handed out most expensive first, by the counters of pt_band_cost): the
+    whole metric frame (share 1) and rank 0's share of an 8-way tiling are the same images bit for bit;
+    the per-band counters add up to the frame's ray segments."""
+    import bench
+    wl = bench.Workload("metric")
+    r = bench_gpu
+    r.upload(wl.scene, wl.cfg)
+    r.setup_frame(wl.width, wl.height)
+    r.set_tiling(bench.BAND_ROWS, share, 0)
+    try:
+        r.stats_reset()
+        r.render(wl.cam, wl.cfg, 1, 8, write_u8=2)
+        r.synchronize()
+        segments = r.stats()["segments"]
+        full, full8 = r.download()
+        order = r.order_bands_by_cost(wl.cam, wl.cfg, 8)
+        n, partial = r.band_count()
+        assert sorted(order) == list(range(n)) and order != list(range(n))
+        r.measure_band_cost(True)
+        r.render(wl.cam, wl.cfg, 1, 1, write_u8=2)  # overwrite with a different frame, counting
+        assert not np.array_equal(r.download()[0], full)
+        one_pass = sum(r.band_cost())
+        r.measure_band_cost(False)
+        r.stats_reset()
+        r.render(wl.cam, wl.cfg, 1, 8, write_u8=2)
+        r.synchronize()
+        assert r.stats()["segments"] == segments
+        img, img8 = r.download()
+        assert 0 < one_pass < segments
+    finally:
+        r.set_band_order(None)
+        r.set_tiling(bench.BAND_ROWS, 1, 0)
+    assert np.array_equal(img, full) and np.array_equal(img8, full8)
+    with pytest.raises(RuntimeError):
+        bad = list(order)
+        bad[0] = bad[1]
+        r.set_tiling(bench.BAND_ROWS, share, 0)
+        r.set_band_order(bad)
+    r.set_tiling(bench.BAND_ROWS, 1, 0)
+
+
 @pytest.mark.parametrize("bands", [4, 8])
 def test_c4_band_tiling_partitions_the_frame(bench_gpu, c4_workload, bands):
     """The multi-GPU partition on the C4 scene at the bench's 8-row bands: every rank's share rendered

@@ -26,6 +26,7 @@ def main() -> None:
     ap.add_argument("--inflight", type=int, default=1, help="frames in flight (one renderer context each)")
     ap.add_argument("--ranks-max", type=int, default=8, help="time at most this many ranks per N")
     ap.add_argument("--share", type=int, default=100, help="pt_set_grid_share: percent of the grid per launch")
+    ap.add_argument("--order", action="store_true", help="hand out bands most expensive first (pt_set_band_order)")
     args = ap.parse_args()
     wl = bench.Workload("metric")
     rs = []
@@ -43,6 +44,8 @@ def main() -> None:
         for k in range(min(n, args.ranks_max)):
             for q in rs:
                 q.set_tiling(bench.BAND_ROWS, n, k)
+                if args.order:
+                    q.order_bands_by_cost(wl.cam, wl.cfg, wl.spp)
                 q.render(wl.cam, wl.cfg, 1, wl.spp, write_u8=0)  # warm
                 q.synchronize()
                 q.stats_reset()
