@@ -72,19 +72,57 @@ struct SceneStage {
     int leaf_size = 1;
 };
 
-template <class T>
-bool same_bytes(const std::vector<T>& a, const std::vector<T>& b) {
-    return a.size() == b.size() && (a.empty() || std::memcmp(a.data(), b.data(), a.size() * sizeof(T)) == 0);
-}
+// 256-bit digest of a translation (the quantised and wide records derive from the rest). Four
+// independent 64-bit lanes over interleaved 8-byte words, each a multiply-xorshift chain with its own
+// constants, every array's length mixed in; DevMaterial records are zero-filled before their fields
+// are set, so padding is deterministic. Change detection for the caller's own uploads, not a defence
+// against crafted collisions.
+struct StageDigest {
+    uint64_t h[4];
+    bool operator==(const StageDigest& o) const { return std::memcmp(h, o.h, sizeof(h)) == 0; }
+};
 
-// Two translations of the reference structures are the same scene (the quantised nodes derive
-// from the rest). DevMaterial records are zero-filled before their fields are set, so padding compares.
-bool same_stage(const SceneStage& a, const SceneStage& b) {
-    return a.cube_len == b.cube_len && a.leaf_size == b.leaf_size && same_bytes(a.nodes, b.nodes) &&
-           same_bytes(a.leaf_tris, b.leaf_tris) && same_bytes(a.mesh_range, b.mesh_range) &&
-           same_bytes(a.tri_geom, b.tri_geom) && same_bytes(a.tri_shade, b.tri_shade) && same_bytes(a.spheres, b.spheres) &&
-           same_bytes(a.mats, b.mats) && same_bytes(a.tex_desc, b.tex_desc) && same_bytes(a.tex_pool, b.tex_pool) &&
-           same_bytes(a.cube, b.cube);
+struct Digester {
+    uint64_t h[4] = {0x243f6a8885a308d3ull, 0x13198a2e03707344ull, 0xa4093822299f31d0ull, 0x082efa98ec4e6c89ull};
+    static uint64_t mix(uint64_t x, uint64_t k) {
+        x ^= x >> 29;
+        x *= k;
+        return x ^ (x >> 32);
+    }
+    void word(int lane, uint64_t w) {
+        static const uint64_t K[4] = {0x9e3779b97f4a7c15ull, 0xbf58476d1ce4e5b9ull, 0x94d049bb133111ebull, 0xff51afd7ed558ccdull};
+        h[lane] = mix(h[lane] ^ w, K[lane]) + 0x632be59bd9b4e019ull;
+    }
+    void bytes(const void* p, size_t n) {
+        const unsigned char* b = static_cast<const unsigned char*>(p);
+        size_t i = 0;
+        for (; i + 32 <= n; i += 32) {
+            uint64_t w[4];
+            std::memcpy(w, b + i, 32);
+            word(0, w[0]); word(1, w[1]); word(2, w[2]); word(3, w[3]);
+        }
+        for (int lane = 0; i < n; lane = (lane + 1) & 3) {
+            uint64_t w = 0;
+            const size_t k = n - i < 8 ? n - i : 8;
+            std::memcpy(&w, b + i, k);
+            word(lane, w);
+            i += k;
+        }
+        for (int lane = 0; lane < 4; lane++) word(lane, (uint64_t)n);
+    }
+    template <class T>
+    void vec(const std::vector<T>& v) { bytes(v.data(), v.size() * sizeof(T)); }
+};
+
+StageDigest stage_digest(const SceneStage& a) {
+    Digester d;
+    const int head[2] = {a.cube_len, a.leaf_size};
+    d.bytes(head, sizeof(head));
+    d.vec(a.nodes); d.vec(a.leaf_tris); d.vec(a.mesh_range); d.vec(a.tri_geom); d.vec(a.tri_shade);
+    d.vec(a.spheres); d.vec(a.mats); d.vec(a.tex_desc); d.vec(a.tex_pool); d.vec(a.cube);
+    StageDigest out;
+    for (int i = 0; i < 4; i++) out.h[i] = Digester::mix(d.h[i] ^ d.h[(i + 1) & 3], 0xd6e8feb86659fd93ull);
+    return out;
 }
 
 DevMaterial to_dev(const pt_material& m) {
@@ -450,8 +488,8 @@ struct pt_context {
     int node_num = 0, tri_num = 0, wide_num = 0;
     bool has_scene = false;
     int material_num = 0;
-    int scene_feat = PT_FEAT_ALL;
-    std::string last_kernel;       // the pass kernel of the last render (pt_last_kernel)  // features the resident scene's materials can reach (pt_path.h PT_FEAT_*)
+    int scene_feat = PT_FEAT_ALL;  // features the resident scene's materials can reach (pt_path.h PT_FEAT_*)
+    std::string last_kernel;       // the pass kernel of the last render (pt_last_kernel)
     float mat_air_n = 0.0f;       // air index the per-material constants were computed for
     bool mat_air_n_valid = false;
     // frame
@@ -499,9 +537,11 @@ struct pt_context {
     int key_counts[2] = {-1, -1};
     // reference-ABI host mirrors
     const void* mirror_host = nullptr;
-    // host copy of the resident scene's translation: an upload of identical content (the reference
-    // caller re-sends the scene on every pass_counter == 1, i.e. after every camera move) keeps it
-    std::unique_ptr<SceneStage> resident;
+    // digest of the resident scene's translation: an upload of identical content (the reference
+    // caller re-sends the scene on every pass_counter == 1, i.e. after every camera move) keeps it.
+    // A digest, not a host copy, so a context holds no second copy of the scene on the host.
+    bool resident_valid = false;
+    StageDigest resident{};
     std::vector<int2> mesh_range;  // node range per mesh of the resident scene
     // pt_mesh_attach: per mesh, device copies of its mesh-local triangles (v0..v2, n0..n2 as float4) and
     // initial node corners, and the inverse of the transform of those boxes
@@ -1033,16 +1073,19 @@ extern "C" int pt_scene_upload(pt_context* ctx, int mesh_num, pt_bvh_node_device
                          mesh_textures, texture_num, config);
     if (rc != PT_OK) return rc;
     const double t_translate = ms();
-    if (ctx->has_scene && ctx->resident && same_stage(*ctx->resident, *st)) {
+    const StageDigest dg = stage_digest(*st);
+    if (ctx->has_scene && ctx->resident_valid && ctx->resident == dg) {
         if (timing) std::fprintf(stderr, "[pt] scene upload: translate %.2f ms, unchanged (%.2f ms)\n", t_translate, ms());
         return PT_OK;
     }
     quantise_nodes(*st);
     build_wide(*st);
+    ctx->resident_valid = false;
     rc = upload_stage(ctx, *st);
     if (timing) std::fprintf(stderr, "[pt] scene upload: translate %.2f ms, quantise+upload -> %.2f ms\n", t_translate, ms());
-    if (rc != PT_OK) { ctx->resident.reset(); return rc; }
-    ctx->resident = std::move(st);
+    if (rc != PT_OK) return rc;
+    ctx->resident = dg;
+    ctx->resident_valid = true;
     return PT_OK;
 }
 
@@ -1130,7 +1173,7 @@ extern "C" int pt_mesh_set_transform(pt_context* ctx, int mesh, pt_float3 positi
                              const_cast<float4*>(ctx->scene.tri_geom), const_cast<float4*>(ctx->scene.tri_shade),
                              const_cast<float4*>(ctx->scene.nodes), ctx->stream));
     ctx->refitted = true;
-    ctx->resident.reset();  // the resident scene no longer equals its last upload
+    ctx->resident_valid = false;  // the resident scene no longer equals its last upload
     std::memset(ctx->grid, 0, sizeof(ctx->grid));
     return PT_OK;
 }
