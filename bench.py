@@ -251,10 +251,20 @@ def main() -> int:
 
     nframe = 0
 
+    last_full = os.environ.get("PT_BENCH_LAST_FULL", "1") != "0"
+
     def run(k: int) -> None:
+        # the last frame of a batch has no frame behind it to fill the CUs its launch leaves: it takes
+        # the whole grid (every frame is still rendered completely, in order, on its own context)
         nonlocal nframe
-        for _ in range(k):
-            frames[nframe % inflight].launch(cam, cfg, spp)
+        for i in range(k):
+            q = frames[nframe % inflight]
+            full = last_full and grid_share < 100 and i == k - 1
+            if full:
+                rs[nframe % inflight].set_grid_share(100)
+            q.launch(cam, cfg, spp)
+            if full:
+                rs[nframe % inflight].set_grid_share(grid_share)
             nframe += 1
 
     run(args.warmup)

@@ -378,7 +378,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     bool a2 = shade_hit<false>(sc, cfg, d2, pseed, &p2, h2, &none);
                     opaque(p2); opaque(a2);
                 }
-                alive = shade_hit<false, FEAT>(sc, cfg, depth, pseed, &ps, h, &none, PROF ? prof + 11 : nullptr);
+                alive = shade_hit<false, FEAT>(sc, cfg, depth, pseed, &ps, h, &none, nullptr);
             }
             if (PROF) tc2 = __builtin_readcyclecounter();
             if (mode == LANE_READY) {  // the pass's end for this unit, or the next trace step
@@ -418,7 +418,12 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         float4 pta = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ptb = pta, ptc = pta;
         for (int k = 0; k < walk_steps; k++) {
             if (k > 0 && !__any(mode == LANE_WALK || mode == LANE_TRI)) break;
-            if (PROF) { prof[1]++; prof[2] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK)); }
+            if (PROF) {
+                prof[1]++; prof[2] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK));
+                prof[12] += (unsigned long long)__popcll(__ballot(mode == LANE_TRI));
+                prof[13] += (unsigned long long)__popcll(__ballot(mode == LANE_READY));
+                prof[14] += (unsigned long long)__popcll(__ballot(mode == LANE_WANT || mode == LANE_DONE));
+            }
             if (mode == LANE_WALK) {
                 if (PT_DUP == 2) {
                     MeshWalk w2 = w; v3 o2 = ps.o, i2 = inv; int t2 = ptri;

@@ -10,7 +10,7 @@ for round in 1 2; do
   for cfg in "$@"; do
     i=$((i+1))
     envs=""; [ "$cfg" != "-" ] && envs="$cfg"
-    env $envs timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/$TAG/b${round}_$i.json 2> gpurun_out/$TAG/b${round}_$i.err || exit $?
+    env $envs timeout -k 10 300 python bench.py --no-cpu-baseline --steps ${STEPS:-10} --warmup ${WARMUP:-3} > gpurun_out/$TAG/b${round}_$i.json 2> gpurun_out/$TAG/b${round}_$i.err || exit $?
     python -c "import json; d=json.load(open('gpurun_out/$TAG/b${round}_$i.json')); print('round $round [$cfg]', d['value'], d['ms_per_step'], d['config']['ms_per_frame_latency'], d['roofline']['avg_launch_ms'])"
   done
 done

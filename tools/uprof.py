@@ -51,8 +51,7 @@ if os.environ.get("PT_REGROUP") == "1":
     print(json.dumps(d))
     sys.exit(0)
 names = ["rounds", "walk_steps", "walking_lanes", "shade_batches", "lanes_shaded", "tri_batches", "tri_lanes", "refilled",
-         "cyc_refill", "cyc_shade", "cyc_walk", "shade_cyc_medium", "shade_cyc_hit_or_miss", "shade_cyc_fresnel",
-         "shade_cyc_bounce", "shade_cyc_next_segment"]
+         "cyc_refill", "cyc_shade", "cyc_walk", "unused", "parked_lanes", "ready_lanes", "idle_lanes", "cyc_next_segment"]
 d = {n: v[16 + i] for i, n in enumerate(names)}
 d["segments"] = v[0]
 d["lanes_per_walk_step"] = round(d["walking_lanes"] / max(d["walk_steps"], 1), 2)
@@ -64,6 +63,7 @@ for k in ("cyc_refill", "cyc_shade", "cyc_walk"):
     d[k.replace("cyc", "frac")] = round(d[k] / max(tot, 1), 3)
 d["cyc_per_walk_round"] = round(d["cyc_walk"] / max(d["rounds"] - d["shade_batches"], 1))
 d["cyc_per_shade_batch"] = round(d["cyc_shade"] / max(d["shade_batches"], 1))
-for k in ("shade_cyc_medium", "shade_cyc_hit_or_miss", "shade_cyc_fresnel", "shade_cyc_bounce", "shade_cyc_next_segment"):
-    d[k.replace("shade_cyc", "shade_frac")] = round(d[k] / max(d["cyc_shade"], 1), 3)
+for k in ("parked_lanes", "ready_lanes", "idle_lanes"):
+    d[k + "_per_walk_step"] = round(d[k] / max(d["walk_steps"], 1), 2)
+d["next_segment_frac_of_shade"] = round(d["cyc_next_segment"] / max(d["cyc_shade"], 1), 3)
 print(json.dumps(d))
