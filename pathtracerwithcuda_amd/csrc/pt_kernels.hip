@@ -176,7 +176,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
 // which a surviving path starts its next segment (spheres, mesh 0) and an ended one takes a new
 // pixel. Every lane still computes exactly the reference sequence for its path (same node order,
 // same tests, same draws keyed by (pass, pixel, depth)); only the interleaving between lanes changes.
-enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3, LANE_TRI = 4 };
+enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3, LANE_TRI = 4, LANE_NEW = 5 };
 
 // Starts the walk of the first mesh at or after `mesh` with a non-empty node range. The ranges of the
 // first PT_LDS_MESHES meshes come from the workgroup's LDS copy (lds_mesh, filled at kernel start), the
@@ -261,10 +261,44 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
     }
 }
 
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// ---- the tail pool of pass_kernel_u -----------------------------------------------------------------
+// Once a launch's work is drained, every wave runs until its last path ends, with fewer and fewer lanes
+// busy: 18 % of the bench frame's walk steps come after the drain, with 8 of 64 lanes walking (PT_UPROF).
+// So a drained wave other than wave 0 of its workgroup that holds at most donor_max paths hands each
+// path that survives a shading batch to its part of a workgroup pool in LDS (the path state at a segment
+// boundary: 64 B) and lets the lane go; such a wave ends early and its SIMD slot serves the next frame
+// in flight. Wave 0 takes pooled paths into its free lanes and ends only when every other wave has
+// ended and the pool is empty. A path continues exactly where it stopped (same state, same draws keyed
+// by (pass, pixel, depth)), so results are unchanged. Slot protocol as pass_kernel_r: a FREE slot
+// belongs to its donor wave, a FULL one to wave 0; data stores complete before the state store.
+#define PT_TP_PART 32                               // pool slots per donor wave
+#define PT_TP_SLOTS (PT_TP_PART * (PT_UBLOCK / 64 - 1))
+template <int N>
+__device__ __forceinline__ void tp_put(float4 (*q)[N], int s, const PathState& ps, unsigned int unit, int32_t pseed,
+                                       int depth) {
+    q[0][s] = make_float4(ps.o.x, ps.o.y, ps.o.z, ps.d.x);
+    q[1][s] = make_float4(ps.d.y, ps.d.z, ps.thr.x, ps.thr.y);
+    q[2][s] = make_float4(ps.thr.z, ps.rad.x, ps.rad.y, ps.rad.z);
+    q[3][s] = make_float4(__uint_as_float(unit), __int_as_float(pseed), __int_as_float(ps.medium), __int_as_float(depth));
+}
+template <int N>
+__device__ __forceinline__ void tp_get(float4 (*q)[N], int s, PathState& ps, unsigned int& unit, int32_t& pseed,
+                                       int& depth) {
+    const float4 a = q[0][s], b = q[1][s], c = q[2][s], e = q[3][s];
+    ps.o = mk3(a.x, a.y, a.z);
+    ps.d = mk3(a.w, b.x, b.y);
+    ps.thr = mk3(b.z, b.w, c.x);
+    ps.rad = mk3(c.y, c.z, c.w);
+    unit = __float_as_uint(e.x); pseed = __float_as_int(e.y); ps.medium = __float_as_int(e.z); depth = __float_as_int(e.w);
+}
+
 // PROF: wave-level occupancy counters of the state machine into stats[16..23] (tools/uprof.py):
 // rounds, walk steps, walking lanes summed over steps, shading batches, lanes shaded, triangle
 // batches, lanes in triangle batches, lanes refilled.
-template <int MINW, bool PROF, bool QN, int CHAIN, bool PF, bool WIDE, int FEAT = PT_FEAT_ALL>
+// TP: the kernel has the tail pool (PT_TAIL_POOL > 0 selects it).
+template <int MINW, bool PROF, bool QN, int CHAIN, bool PF, bool WIDE, int FEAT = PT_FEAT_ALL, bool TP = false>
 __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
                                                                 int walk_steps, int tri_min, int walk_min, int tail) {
@@ -275,12 +309,22 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     // reserves their bytes of dynamic LDS; pass_kernel_u runs only when that fits, PT_LDS_TABLES)
     __shared__ int2 lds_mesh[PT_LDS_MESHES];
     __shared__ int lds_wroot[WIDE ? PT_LDS_MESHES : 1];
+    __shared__ float4 tp_q[4][TP ? PT_TP_SLOTS : 1];
+    __shared__ int tp_state[TP ? PT_TP_SLOTS : 1];        // 0 free, 1 full
+    __shared__ int tp_scr[PT_UBLOCK / 64][TP ? PT_TP_SLOTS : 1];
+    __shared__ int tp_donors;                    // waves other than wave 0 still running
     extern __shared__ float4 lds_dyn[];
     DevMaterial* lds_mats = reinterpret_cast<DevMaterial*>(lds_dyn);
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int donor_max = TP ? (tail >> 16) & 0xff : 0;  // 0: no tail pool
     {
         const int2* mr = uniform_ptr(P0->sc.mesh_range);
         const int n = min(uniform_int(P0->sc.mesh_num), PT_LDS_MESHES);
         for (int i = threadIdx.x; i < n; i += PT_UBLOCK) lds_mesh[i] = mr[i];
+        if (TP) {
+            for (int i = threadIdx.x; i < PT_TP_SLOTS; i += PT_UBLOCK) tp_state[i] = 0;
+            if (threadIdx.x == 0) tp_donors = PT_UBLOCK / 64 - 1;
+        }
         if (WIDE) {
             const int* mw = uniform_ptr(P0->sc.mesh_wide);
             for (int i = threadIdx.x; i < n; i += PT_UBLOCK) lds_wroot[i] = mw[i];
@@ -348,7 +392,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     pseed = path_seed(hseed, pixel);
                     depth = 0;
                     if (cfg.max_depth > 0) {
-                        mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
+                        mode = LANE_NEW;
                     } else {
                         finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
                     }
@@ -357,6 +401,45 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 }
             }
         }
+        if (TP && donor_max && wid == 0 && drained) {
+            // wave 0 takes pooled paths into its free lanes (see the tail pool above); with no path in
+            // any lane it waits here until the pool has one or every other wave has ended
+            const unsigned long long freem = __ballot(mode == LANE_DONE);
+            if (freem) {
+                volatile int* tst = tp_state;
+                int v0, v1, n0, nfull;
+                unsigned long long f0, f1;
+                while (true) {
+                    const int donors_left = *(volatile int*)&tp_donors;
+                    lds_fence();  // the pool is scanned after the count is read
+                    v0 = lane < PT_TP_SLOTS ? tst[lane] : 0;
+                    v1 = lane + 64 < PT_TP_SLOTS ? tst[lane + 64] : 0;
+                    f0 = __ballot(v0 == 1);
+                    f1 = __ballot(v1 == 1);
+                    n0 = __popcll(f0);
+                    nfull = n0 + __popcll(f1);
+                    if (nfull || donors_left == 0 || freem != ~0ull) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (nfull) {
+                    int* scr = tp_scr[0];
+                    const unsigned long long below = lanes_below(lane);
+                    if (v0 == 1) scr[__popcll(f0 & below)] = lane;
+                    if (v1 == 1) scr[n0 + __popcll(f1 & below)] = lane + 64;
+                    lds_fence();
+                    const int k = __popcll(freem & below);
+                    int slot = -1;
+                    if (mode == LANE_DONE && k < nfull) {
+                        slot = scr[k];
+                        tp_get(tp_q, slot, ps, unit, pseed, depth);
+                        mode = LANE_NEW;
+                    }
+                    lds_fence();
+                    if (slot >= 0) tst[slot] = 0;
+                }
+            }
+        }
+        if (mode == LANE_NEW) mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
         if (!__any(mode != LANE_DONE)) break;
         if (PROF) { const unsigned long long t = __builtin_readcyclecounter(); prof[8] += t - tc; tc = t; }
 
@@ -387,9 +470,34 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
                     mode = LANE_WANT;
                 } else {
-                    mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
+                    mode = LANE_NEW;
                 }
             }
+            if (TP && donor_max && drained && wid != 0) {
+                // a drained wave with few paths left hands its survivors to the pool (tail pool above)
+                const unsigned long long surv = __ballot(mode == LANE_NEW);
+                const int live = __popcll(__ballot(mode != LANE_DONE && mode != LANE_WANT));
+                if (surv && live <= donor_max) {
+                    volatile int* tst = tp_state;
+                    int* scr = tp_scr[wid];
+                    const unsigned long long below = lanes_below(lane);
+                    const int base = (wid - 1) * PT_TP_PART;
+                    const int sv = lane < PT_TP_PART ? tst[base + lane] : 1;
+                    const unsigned long long fr = __ballot(sv == 0);
+                    if (sv == 0) scr[__popcll(fr & below)] = base + lane;
+                    lds_fence();
+                    const int r = __popcll(surv & below);
+                    int slot = -1;
+                    if (mode == LANE_NEW && r < __popcll(fr)) {
+                        slot = scr[r];
+                        tp_put(tp_q, slot, ps, unit, pseed, depth);
+                        mode = LANE_DONE;
+                    }
+                    lds_fence();
+                    if (slot >= 0) tst[slot] = 1;
+                }
+            }
+            if (mode == LANE_NEW) mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
             if (PROF) prof[15] += __builtin_readcyclecounter() - tc2;
             if (PROF) prof[9] += __builtin_readcyclecounter() - tc;
             continue;
@@ -421,6 +529,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (PROF) {
                 prof[1]++; prof[2] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK));
                 prof[12] += (unsigned long long)__popcll(__ballot(mode == LANE_TRI));
+                if (drained) prof[11] += 1ull | ((unsigned long long)__popcll(__ballot(mode == LANE_WALK)) << 32);
                 prof[13] += (unsigned long long)__popcll(__ballot(mode == LANE_READY));
                 prof[14] += (unsigned long long)__popcll(__ballot(mode == LANE_WANT || mode == LANE_DONE));
             }
@@ -472,6 +581,10 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         if (PROF) prof[10] += __builtin_readcyclecounter() - tc;
     }
 
+    if (TP && donor_max && wid != 0 && lane == 0) {
+        lds_fence();  // this wave's pool stores before its exit is counted
+        atomicSub(&tp_donors, 1);
+    }
     if (lane == 0) {
         atomicAdd(&P0->out.stats[0], segments);
         if (PROF) {
@@ -501,9 +614,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
 #define PT_RG_PART 64
 #define PT_RG_IDLE_CAP (1 << 24)  // idle rounds after which a wave gives up (never reached by a correct run)
 enum : int { SLOT_FREE = 0, SLOT_WALK = 1, SLOT_SHADE = 2 };
-enum : int { LANE_NEW = 5 };  // walker lane holding a path that starts its next segment
 
-__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // q0 (o, d.x) q1 (d.y, d.z, thr.x, thr.y) q2 (thr.z, rad) q3 (unit, pseed, medium, depth) q4 (hit)
 __device__ __forceinline__ void slot_put(float4* const q[5], int s, const PathState& ps, unsigned int unit, int32_t pseed,
@@ -1066,7 +1177,10 @@ using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int,
 // scene can reach; PT_FEAT_SPECIALISE=0 keeps the all-features kernel.
 static PassFnU pass_fn_feat(int minw, int feat) {
     static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
+    static const int pool = env_int("PT_TAIL_POOL", 0, 0, 64);
     if (!spec) feat = PT_FEAT_ALL;
+    if (pool && minw == 7 && feat == 0) return pass_kernel_u<7, false, false, 2, true, false, 0, true>;
+    if (pool && minw == 6 && feat == PT_FEAT_ALL) return pass_kernel_u<6, false, false, 2, true, false, PT_FEAT_ALL, true>;
     switch (minw * 4 + feat) {
         case 5 * 4 + 0: return pass_kernel_u<5, false, false, 2, true, false, 0>;
         case 5 * 4 + 1: return pass_kernel_u<5, false, false, 2, true, false, 1>;
@@ -1090,13 +1204,15 @@ static PassFnU pass_fn_u(int minw, bool qn, bool wide, int feat) {
     static const int prof = env_int("PT_UPROF", 0, 0, 1);
     static const int chain = env_int("PT_WALK_CHAIN", 2, 1, 3);
     static const int pf = env_int("PT_TRI_PREFETCH", 1, 0, 1);
+    if (prof && env_int("PT_TAIL_POOL", 0, 0, 64) && !qn && !wide)
+        return pass_kernel_u<6, true, false, 2, true, false, PT_FEAT_ALL, true>;
     if (prof) return qn ? pass_kernel_u<6, true, true, 1, false, false>
                         : (wide ? pass_kernel_u<6, true, false, 2, true, true> : pass_kernel_u<6, true, false, 2, true, false>);
     if (qn) return minw == 6 ? pass_kernel_u<6, false, true, 1, false, false> : pass_kernel_u<5, false, true, 1, false, false>;
     if (wide) return minw == 5 ? pass_kernel_u<5, false, false, 2, true, true> : pass_kernel_u<6, false, false, 2, true, true>;
     if (chain == 1) return minw == 6 ? pass_kernel_u<6, false, false, 1, false, false> : pass_kernel_u<5, false, false, 1, false, false>;
     if (chain == 3) return minw == 6 ? pass_kernel_u<6, false, false, 3, false, false> : pass_kernel_u<5, false, false, 3, false, false>;
-    if (pf && feat != PT_FEAT_ALL) {
+    if (pf) {  // specialised on the scene's features, or with the tail pool (nullptr: neither applies)
         PassFnU f = pass_fn_feat(minw, feat);
         if (f) return f;
     }
@@ -1171,8 +1287,11 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, bool
         // PT_TAIL_SHADE_MIN / PT_TAIL_WALK_MIN: the shading thresholds of a wave once the work is drained
         static const int tail_shade = env_int("PT_TAIL_SHADE_MIN", shade_min, 1, 64);
         static const int tail_walk = env_int("PT_TAIL_WALK_MIN", walk_min, 0, 64);
+        // PT_TAIL_POOL: a drained wave holding at most this many paths hands them to wave 0 of its
+        // workgroup (pass_kernel_u's tail pool; 0 = off)
+        static const int tail_pool = env_int("PT_TAIL_POOL", 0, 0, 64);
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
-            a8 = walk_min, a9 = tail_shade | (tail_walk << 8);
+            a8 = walk_min, a9 = tail_shade | (tail_walk << 8) | (tail_pool << 16);
         void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8, &a9};
         hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true, feat), qn, wide && !qn, feat), dim3(grid), dim3(PT_UBLOCK), args,
                                        (size_t)lds_bytes, stream);
@@ -1217,9 +1336,12 @@ std::string pass_kernel_desc(bool leaf1, bool stats, bool qn, bool wide, int fea
         static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
         static const int chain = env_int("PT_WALK_CHAIN", 2, 1, 3);
         static const int pf = env_int("PT_TRI_PREFETCH", 1, 0, 1);
-        std::snprintf(buf, sizeof(buf), "pass_kernel_u<MINW=%d,QN=%d,CHAIN=%d,PF=%d,WIDE=%d,FEAT=%d>",
-                      pass_min_waves(true, feat), qn ? 1 : 0, qn ? 1 : chain, qn ? 0 : pf, wide && !qn ? 1 : 0,
-                      spec && !qn && !wide && pf && chain == 2 ? feat : PT_FEAT_ALL);
+        static const int pool = env_int("PT_TAIL_POOL", 0, 0, 64);
+        const int minw = pass_min_waves(true, feat);
+        const int f = spec && !qn && !wide && pf && chain == 2 ? feat : PT_FEAT_ALL;
+        const bool tp = pool && !qn && !wide && pf && chain == 2 && ((minw == 7 && f == 0) || (minw == 6 && f == PT_FEAT_ALL));
+        std::snprintf(buf, sizeof(buf), "pass_kernel_u<MINW=%d,QN=%d,CHAIN=%d,PF=%d,WIDE=%d,FEAT=%d%s>", minw,
+                      qn ? 1 : 0, qn ? 1 : chain, qn ? 0 : pf, wide && !qn ? 1 : 0, f, tp ? ",TAILPOOL" : "");
     } else {
         std::snprintf(buf, sizeof(buf), "pass_kernel<LEAF1=%d,STATS=%d,MINW=%d,QN=%d>", leaf1 ? 1 : 0, stats ? 1 : 0,
                       pass_min_waves(false, feat), qn ? 1 : 0);

@@ -51,7 +51,7 @@ if os.environ.get("PT_REGROUP") == "1":
     print(json.dumps(d))
     sys.exit(0)
 names = ["rounds", "walk_steps", "walking_lanes", "shade_batches", "lanes_shaded", "tri_batches", "tri_lanes", "refilled",
-         "cyc_refill", "cyc_shade", "cyc_walk", "unused", "parked_lanes", "ready_lanes", "idle_lanes", "cyc_next_segment"]
+         "cyc_refill", "cyc_shade", "cyc_walk", "drained_steps_lanes", "parked_lanes", "ready_lanes", "idle_lanes", "cyc_next_segment"]
 d = {n: v[16 + i] for i, n in enumerate(names)}
 d["segments"] = v[0]
 d["lanes_per_walk_step"] = round(d["walking_lanes"] / max(d["walk_steps"], 1), 2)
@@ -65,5 +65,9 @@ d["cyc_per_walk_round"] = round(d["cyc_walk"] / max(d["rounds"] - d["shade_batch
 d["cyc_per_shade_batch"] = round(d["cyc_shade"] / max(d["shade_batches"], 1))
 for k in ("parked_lanes", "ready_lanes", "idle_lanes"):
     d[k + "_per_walk_step"] = round(d[k] / max(d["walk_steps"], 1), 2)
+d["drained_walk_steps"] = d["drained_steps_lanes"] & 0xffffffff
+d["drained_walking_lanes"] = d.pop("drained_steps_lanes") >> 32
+d["drained_frac_of_walk_steps"] = round(d["drained_walk_steps"] / max(d["walk_steps"], 1), 3)
+d["drained_lanes_per_walk_step"] = round(d["drained_walking_lanes"] / max(d["drained_walk_steps"], 1), 2)
 d["next_segment_frac_of_shade"] = round(d["cyc_next_segment"] / max(d["cyc_shade"], 1), 3)
 print(json.dumps(d))
