@@ -1151,8 +1151,9 @@ static PassFn pass_fn(bool leaf1, bool stats, int minw, bool qn) {
 }
 
 // PT_MIN_WAVES overrides the occupancy target: 8 waves/SIMD for pass_kernel (64 VGPRs); for pass_kernel_u
-// 7 when the scene reaches neither textures nor media (72 VGPRs, no spills: +3.5% over 6 on the bench
-// frame, profiles/r02/feat1) and 6 otherwise (80 VGPRs; at 72 the full kernel spills and loses 5%).
+// 7 when the scene reaches no participating medium (72 VGPRs: no spills without textures, +3.5 % over 6 on
+// the bench frame; one cold spill with textures, +6.7 % on C5) and 6 otherwise (80 VGPRs; at 72 the medium
+// step spills: C4 5049 vs 5378 Mrays/s, profiles/r02/workloads).
 int pass_min_waves(bool unified, int feat) {
     static int w = [] {
         const char* e = getenv("PT_MIN_WAVES");
@@ -1161,7 +1162,7 @@ int pass_min_waves(bool unified, int feat) {
     }();
     if (w) return w;
     if (!unified) return 8;
-    return feat == 0 ? 7 : 6;
+    return (feat & PT_FEAT_MEDIUM) ? 6 : 7;
 }
 
 // PT_UNIFIED=0 selects pass_kernel for the default configuration (leaf size 1, uninstrumented, exact
