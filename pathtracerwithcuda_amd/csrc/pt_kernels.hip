@@ -1338,7 +1338,10 @@ std::string pass_kernel_desc(bool leaf1, bool stats, bool qn, bool wide, int fea
         static const int chain = env_int("PT_WALK_CHAIN", 2, 1, 3);
         static const int pf = env_int("PT_TRI_PREFETCH", 1, 0, 1);
         static const int pool = env_int("PT_TAIL_POOL", 0, 0, 64);
-        const int minw = pass_min_waves(true, feat);
+        int minw = pass_min_waves(true, feat);
+        // the instance pass_fn_u picks for this wave target (not every variant has every target)
+        if (qn || (chain != 2 && !wide) || (!pf && !wide)) minw = minw == 6 ? 6 : 5;
+        else if (wide) minw = minw == 5 ? 5 : 6;
         const int f = spec && !qn && !wide && pf && chain == 2 ? feat : PT_FEAT_ALL;
         const bool tp = pool && !qn && !wide && pf && chain == 2 && ((minw == 7 && f == 0) || (minw == 6 && f == PT_FEAT_ALL));
         std::snprintf(buf, sizeof(buf), "pass_kernel_u<MINW=%d,QN=%d,CHAIN=%d,PF=%d,WIDE=%d,FEAT=%d%s>", minw,
