@@ -173,8 +173,9 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
 // lane is a small state machine: WALK (one BVH node per step of the mesh in flight, then the next
 // mesh), READY (closest hit known) and, for the wave, a SHADE step that runs shade_hit for every
 // READY lane at once — taken when no lane is walking or at least shade_min lanes are ready — after
-// which a surviving path starts its next segment (spheres, mesh 0) and an ended one takes a new
-// pixel. Every lane still computes exactly the reference sequence for its path (same node order,
+// which an ended path takes a new pixel and a surviving one starts its next segment (spheres, mesh 0):
+// both in the next round's refill, so one begin_segment serves new and surviving paths together
+// (+2.5 % over starting survivors inside the shading batch, profiles/r02/onesite.txt). Every lane still computes exactly the reference sequence for its path (same node order,
 // same tests, same draws keyed by (pass, pixel, depth)); only the interleaving between lanes changes.
 enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3, LANE_TRI = 4, LANE_NEW = 5 };
 
@@ -401,6 +402,30 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 }
             }
         }
+        if (TP && donor_max && drained && wid != 0) {
+            // a drained wave with few paths left hands its survivors to the pool (tail pool above)
+            const unsigned long long surv = __ballot(mode == LANE_NEW);
+            const int live = __popcll(__ballot(mode != LANE_DONE && mode != LANE_WANT));
+            if (surv && live <= donor_max) {
+                volatile int* tst = tp_state;
+                int* scr = tp_scr[wid];
+                const unsigned long long below = lanes_below(lane);
+                const int base = (wid - 1) * PT_TP_PART;
+                const int sv = lane < PT_TP_PART ? tst[base + lane] : 1;
+                const unsigned long long fr = __ballot(sv == 0);
+                if (sv == 0) scr[__popcll(fr & below)] = base + lane;
+                lds_fence();
+                const int r = __popcll(surv & below);
+                int slot = -1;
+                if (mode == LANE_NEW && r < __popcll(fr)) {
+                    slot = scr[r];
+                    tp_put(tp_q, slot, ps, unit, pseed, depth);
+                    mode = LANE_DONE;
+                }
+                lds_fence();
+                if (slot >= 0) tst[slot] = 1;
+            }
+        }
         if (TP && donor_max && wid == 0 && drained) {
             // wave 0 takes pooled paths into its free lanes (see the tail pool above); with no path in
             // any lane it waits here until the pool has one or every other wave has ended
@@ -470,34 +495,9 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
                     mode = LANE_WANT;
                 } else {
-                    mode = LANE_NEW;
+                    mode = LANE_NEW;  // its next segment starts in the next round's refill, with the new paths
                 }
             }
-            if (TP && donor_max && drained && wid != 0) {
-                // a drained wave with few paths left hands its survivors to the pool (tail pool above)
-                const unsigned long long surv = __ballot(mode == LANE_NEW);
-                const int live = __popcll(__ballot(mode != LANE_DONE && mode != LANE_WANT));
-                if (surv && live <= donor_max) {
-                    volatile int* tst = tp_state;
-                    int* scr = tp_scr[wid];
-                    const unsigned long long below = lanes_below(lane);
-                    const int base = (wid - 1) * PT_TP_PART;
-                    const int sv = lane < PT_TP_PART ? tst[base + lane] : 1;
-                    const unsigned long long fr = __ballot(sv == 0);
-                    if (sv == 0) scr[__popcll(fr & below)] = base + lane;
-                    lds_fence();
-                    const int r = __popcll(surv & below);
-                    int slot = -1;
-                    if (mode == LANE_NEW && r < __popcll(fr)) {
-                        slot = scr[r];
-                        tp_put(tp_q, slot, ps, unit, pseed, depth);
-                        mode = LANE_DONE;
-                    }
-                    lds_fence();
-                    if (slot >= 0) tst[slot] = 1;
-                }
-            }
-            if (mode == LANE_NEW) mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
             if (PROF) prof[15] += __builtin_readcyclecounter() - tc2;
             if (PROF) prof[9] += __builtin_readcyclecounter() - tc;
             continue;
