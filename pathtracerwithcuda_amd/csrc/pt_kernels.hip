@@ -29,6 +29,9 @@ namespace pt {
 #ifndef PT_DUP
 #define PT_DUP 0
 #endif
+#ifndef PT_MESH_SITE
+#define PT_MESH_SITE 1
+#endif
 template <class T>
 __device__ __forceinline__ void opaque(T& x) {
     int* p = reinterpret_cast<int*>(&x);
@@ -549,7 +552,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     if (PF && !QN) {  // the triangle's loads are in flight while the batch fills
                         pta = bload(rt, ptri * 48); ptb = bload(rt, ptri * 48 + 16); ptc = bload(rt, ptri * 48 + 32);
                     }
-                } else if (w.pos == w.end) {
+                } else if (!PT_MESH_SITE && w.pos == w.end) {
                     mesh_done();
                 }
             }
@@ -574,9 +577,12 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                         else walk_tri(rt, ps.o, ps.d, w, ptri, advance);
                     }
                     mode = LANE_WALK;
-                    if (w.pos == w.end) mesh_done();
+                    if (!PT_MESH_SITE && w.pos == w.end) mesh_done();
                 }
             }
+            // a lane whose mesh walk ended in this step (after a box or after its triangle) merges it and
+            // starts the next mesh: one mesh_done site for both (PT_MESH_SITE=0 builds: two)
+            if (PT_MESH_SITE && mode == LANE_WALK && w.pos == w.end) mesh_done();
         }
         if (PROF) prof[10] += __builtin_readcyclecounter() - tc;
     }
