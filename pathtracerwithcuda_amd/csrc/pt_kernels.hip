@@ -486,7 +486,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 if (PT_DUP == 1) {
                     PathState p2 = ps; Hit h2 = h; int d2 = depth;
                     opaque(p2); opaque(h2); opaque(d2);
-                    bool a2 = shade_hit<false>(sc, cfg, d2, pseed, &p2, h2, &none);
+                    bool a2 = shade_hit<false, FEAT>(sc, cfg, d2, pseed, &p2, h2, &none, nullptr);
                     opaque(p2); opaque(a2);
                 }
                 alive = shade_hit<false, FEAT>(sc, cfg, depth, pseed, &ps, h, &none, nullptr);
