@@ -32,6 +32,10 @@ namespace pt {
 #ifndef PT_MESH_SITE
 #define PT_MESH_SITE 1
 #endif
+// PT_NEXT_MESH: mesh changes read the LDS next-mesh table (start_mesh_next); 0: the mesh loop
+#ifndef PT_NEXT_MESH
+#define PT_NEXT_MESH 1
+#endif
 template <class T>
 __device__ __forceinline__ void opaque(T& x) {
     int* p = reinterpret_cast<int*>(&x);
@@ -217,6 +221,20 @@ __device__ __forceinline__ bool start_mesh(const DevScene& sc, const int2* lds_m
     return false;
 }
 
+// start_mesh for scenes of at most PT_LDS_MESHES meshes walking the binary nodes: lds_next[m] holds the
+// range and index of the first non-empty mesh at or after m (index mesh_num and an empty range: none
+// left), built at kernel start. One LDS read and no loop: a mesh change in a walk step then waits only
+// on LDS, not on the wave's outstanding vector loads (the looping version's mixed LDS / buffer-load
+// path made it wait for every one, parked lanes' triangle prefetches included).
+__device__ __forceinline__ bool start_mesh_next(const int4* lds_next, int& mesh, MeshWalk& w) {
+    const int4 e = lds_next[mesh];
+    mesh = e.z;
+    if (e.x == e.y) return false;
+    w.pos = e.x; w.end = e.y;
+    w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
+    return true;
+}
+
 // Start of one trace_ray_kernel invocation (path_tracer_kernel.cu:418-454): brute-force spheres into
 // the closest hit, then the walk of mesh 0. WIDE scenes: a lane whose 1/d is finite walks the wide
 // records, any other the binary nodes (walk_wide's exactness needs a finite 1/d).
@@ -313,6 +331,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     // reserves their bytes of dynamic LDS; pass_kernel_u runs only when that fits, PT_LDS_TABLES)
     __shared__ int2 lds_mesh[PT_LDS_MESHES];
     __shared__ int lds_wroot[WIDE ? PT_LDS_MESHES : 1];
+    __shared__ int4 lds_next[PT_LDS_MESHES + 1];
     __shared__ float4 tp_q[4][TP ? PT_TP_SLOTS : 1];
     __shared__ int tp_state[TP ? PT_TP_SLOTS : 1];        // 0 free, 1 full
     __shared__ int tp_scr[PT_UBLOCK / 64][TP ? PT_TP_SLOTS : 1];
@@ -340,6 +359,14 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         const int ns = uniform_int(P0->sc.sphere_num) * 2;
         for (int i = threadIdx.x; i < ns; i += PT_UBLOCK) lds_dyn[nm + i] = sp[i];
         __syncthreads();
+        if (uniform_int(P0->sc.mesh_num) <= PT_LDS_MESHES) {  // lds_next (start_mesh_next)
+            for (int i = threadIdx.x; i <= n; i += PT_UBLOCK) {
+                int j = i;
+                while (j < n && lds_mesh[j].x == lds_mesh[j].y) j++;
+                lds_next[i] = j < n ? make_int4(lds_mesh[j].x, lds_mesh[j].y, j, 0) : make_int4(0, 0, n, 0);
+            }
+            __syncthreads();
+        }
     }
     const float4* lds_spheres = lds_dyn + uniform_int(P0->sc.material_num) * (int)(sizeof(DevMaterial) / 16);
 
@@ -522,7 +549,10 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 h.t = w.t; h.t1 = w.t1; h.t2 = w.t2; h.prim = w.tri; h.type = 2;
             }
             mesh++;
-            mode = start_mesh(sc, lds_mesh, lds_wroot, WIDE && w.end < 0, mesh, w) ? LANE_WALK : LANE_READY;
+            bool more;
+            if (PT_NEXT_MESH && !WIDE && sc.mesh_num <= PT_LDS_MESHES) more = start_mesh_next(lds_next, mesh, w);
+            else more = start_mesh(sc, lds_mesh, lds_wroot, WIDE && w.end < 0, mesh, w);
+            mode = more ? LANE_WALK : LANE_READY;
         };
         // PF: the parked triangle's geometry, loaded at the park; scoped to the walk loop, which no lane
         // leaves parked (the last step flushes the batch), so it is not live across shading
