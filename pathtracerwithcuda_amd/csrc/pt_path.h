@@ -841,15 +841,18 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
         mid = f2i(sc.spheres[2 * h.prim + 1].x);
         normal = normalize(point - mk3(s.x, s.y, s.z));
     } else {
-        const float4* sh = sc.tri_shade + 4 * h.prim;
-        float4 s0 = sh[0], s1 = sh[1], s2 = sh[2];
-        mid = f2i(sh[3].w);
+        // the hit record's four 16-B loads through a buffer descriptor, issued together: the material id
+        // (s3.w) arrives with the normals (a generic pointer here let the compiler merge it with the
+        // sphere branch's LDS read into one flat load, a second round trip waiting on both counters)
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(sc.tri_shade, sc.tri_count * 64);
+        const float4 s0 = bload(rs, h.prim * 64), s1 = bload(rs, h.prim * 64 + 16), s2 = bload(rs, h.prim * 64 + 32),
+                     s3 = bload(rs, h.prim * 64 + 48);
+        mid = f2i(s3.w);
         v3 n0 = mk3(s0.x, s0.y, s0.z), n1 = mk3(s0.w, s1.x, s1.y), n2 = mk3(s1.z, s1.w, s2.x);
         float w = 1.0f - h.t1 - h.t2;
         normal = n0 * w + n1 * h.t1 + n2 * h.t2;
         const DevMaterial& M = sc.materials[mid];
         if ((FEAT & PT_FEAT_TEX) && (M.diffuse_texture_id != -1 || M.specular_texture_id != -1)) {
-            float4 s3 = sh[3];
             v2 uv0 = mk2(s2.y, s2.z), uv1 = mk2(s2.w, s3.x), uv2 = mk2(s3.y, s3.z);
             uv = uv0 * w + uv1 * h.t1 + uv2 * h.t2;
             textured = true;

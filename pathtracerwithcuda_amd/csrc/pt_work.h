@@ -27,12 +27,19 @@ __device__ __forceinline__ unsigned long long lanes_below(int lane) {
 // Unit u of this launch's share of the frame -> pixel index (DevTiling: bands of band_rows rows
 // dealt round-robin over band_count owners).
 __device__ __forceinline__ int unit_to_pixel(const DevTiling& til, unsigned int u) {
-    if (til.band_count == 1 && !til.band_order) return (int)u;
+    if (til.band_order) {  // bands handed out by cost (pt_set_band_order); its load is waited for in here
+        const int row_local = (int)u / til.width;
+        const int x = (int)u - row_local * til.width;
+        const int band_local = row_local / til.band_rows;
+        const int row_in_band = row_local - band_local * til.band_rows;
+        const int b = __builtin_nontemporal_load(til.band_order + band_local);
+        return ((b * til.band_count + til.band_index) * til.band_rows + row_in_band) * til.width + x;
+    }
+    if (til.band_count == 1) return (int)u;
     int row_local = (int)u / til.width;
     int x = (int)u - row_local * til.width;
     int band_local = row_local / til.band_rows;
     int row_in_band = row_local - band_local * til.band_rows;
-    if (til.band_order) band_local = til.band_order[band_local];  // bands handed out by cost (pt_set_band_order)
     int y = (band_local * til.band_count + til.band_index) * til.band_rows + row_in_band;
     return y * til.width + x;
 }
