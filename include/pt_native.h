@@ -50,6 +50,9 @@ int pt_set_regroup(pt_context* ctx, int mode);
  * with several contexts rendering frames in flight, the rest of the CUs run the other frames
  * (DESIGN.md §6). Results do not depend on it. */
 int pt_set_grid_share(pt_context* ctx, int percent);
+/* pass_kernel_u's tail pool: once the work is drained, a wave holding at most `paths`
+ * paths hands them to wave 0 of its workgroup and ends. 0: off (default), -1: PT_TAIL_POOL. Same results. */
+int pt_set_tail_pool(pt_context* ctx, int paths);
 /* Band order of the work queue. The context's pixels are bands of band_rows rows
  * (pt_set_tiling; one context: bands of the whole frame). pt_band_count gives their number and whether
  * the last is partial; pt_set_band_order(order, n) hands out local band order[i] i-th (a permutation

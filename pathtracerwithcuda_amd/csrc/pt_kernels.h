@@ -20,11 +20,18 @@
 
 namespace pt {
 
-// regroup: run pass_kernel_r (walker and shader waves) where pass_kernel_u would run, when the scene
-// walks the exact binary nodes (no quantised or wide records)
-hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, bool wide, int feat, bool regroup,
-                       int first_pass, int batch_log2, int write_u8, int grid, bool stats, int lds_bytes,
-                       hipStream_t stream);
+// Which pass kernel a render launches (pt_runtime.cpp pass_choice): leaf size 1, instrumented, quantised
+// or wide records, the scene's reachable features; regroup: pass_kernel_r (walker and shader waves)
+// where pass_kernel_u would run on the exact binary nodes; tail_pool > 0: pass_kernel_u with the tail
+// pool, a drained wave holding at most tail_pool paths hands them to wave 0 of its workgroup.
+struct PassChoice {
+    bool leaf1, stats, qn, wide;
+    int feat;
+    bool regroup;
+    int tail_pool;
+};
+hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int first_pass, int batch_log2,
+                       int write_u8, int grid, int lds_bytes, hipStream_t stream);
 hipError_t launch_accumulate(const LaunchParams* params_dev, int units, int first_pass, int batch_log2, int write_u8,
                              hipStream_t stream);
 hipError_t launch_extend(const LaunchParams* P, bool gen, bool leaf1, bool stats, int depth, int pass, hipStream_t s);
@@ -33,10 +40,8 @@ int shade_grid_waves();
 hipError_t launch_finalize(const LaunchParams* P, int units, int pass, int write_u8, int traced, hipStream_t s);
 hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256, int pixel_count, int pass,
                      hipStream_t stream);
-int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int feat, bool regroup, int lds_bytes);
-// lds_bytes: pass_kernel_u's dynamic LDS
-std::string pass_kernel_desc(bool leaf1, bool stats, bool qn, bool wide, int feat, bool regroup, int lds_bytes);
-bool regroup_applies(bool leaf1, bool stats, bool qn, bool wide, int lds_bytes);
+int pass_grid_size(const PassChoice& pc, int lds_bytes);  // lds_bytes: pass_kernel_u's dynamic LDS
+std::string pass_kernel_desc(const PassChoice& pc, int lds_bytes);
 int env_int(const char* name, int dflt, int lo, int hi);  // clamped integer from the environment
 hipError_t launch_material_consts(DevMaterial* mats, int n, float air_n, hipStream_t stream);
 hipError_t launch_mesh_refit(const float4* local, int tri_start, int tri_count, const float4* init_nodes, int node_first,

@@ -1212,12 +1212,12 @@ using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int,
 
 // The product configuration specialised on the scene's features (pt_path.h PT_FEAT_*): feat is what the
 // scene can reach; PT_FEAT_SPECIALISE=0 keeps the all-features kernel.
-static PassFnU pass_fn_feat(int minw, int feat) {
+static PassFnU pass_fn_feat(int minw, int feat, int pool) {
     static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
-    static const int pool = env_int("PT_TAIL_POOL", 0, 0, 64);
     if (!spec) feat = PT_FEAT_ALL;
+    // tail pool: the bench scene's instance, else the all-features one
     if (pool && minw == 7 && feat == 0) return pass_kernel_u<7, false, false, 2, true, false, 0, true>;
-    if (pool && minw == 6 && feat == PT_FEAT_ALL) return pass_kernel_u<6, false, false, 2, true, false, PT_FEAT_ALL, true>;
+    if (pool) return pass_kernel_u<6, false, false, 2, true, false, PT_FEAT_ALL, true>;
     switch (minw * 4 + feat) {
         case 5 * 4 + 0: return pass_kernel_u<5, false, false, 2, true, false, 0>;
         case 5 * 4 + 1: return pass_kernel_u<5, false, false, 2, true, false, 1>;
@@ -1237,11 +1237,11 @@ static PassFnU pass_fn_feat(int minw, int feat) {
 
 // PT_WALK_CHAIN: records per binary walk step (walk_box_chain); 1 = walk_box. wide: the scene has wide
 // records and PT_WIDE (default 0) allows their walk (walk_wide). feat: the scene's reachable features.
-static PassFnU pass_fn_u(int minw, bool qn, bool wide, int feat) {
+static PassFnU pass_fn_u(int minw, bool qn, bool wide, int feat, int pool) {
     static const int prof = env_int("PT_UPROF", 0, 0, 1);
     static const int chain = env_int("PT_WALK_CHAIN", 2, 1, 3);
     static const int pf = env_int("PT_TRI_PREFETCH", 1, 0, 1);
-    if (prof && env_int("PT_TAIL_POOL", 0, 0, 64) && !qn && !wide)
+    if (prof && pool && !qn && !wide)
         return pass_kernel_u<6, true, false, 2, true, false, PT_FEAT_ALL, true>;
     if (prof) return qn ? pass_kernel_u<6, true, true, 1, false, false>
                         : (wide ? pass_kernel_u<6, true, false, 2, true, true> : pass_kernel_u<6, true, false, 2, true, false>);
@@ -1250,7 +1250,7 @@ static PassFnU pass_fn_u(int minw, bool qn, bool wide, int feat) {
     if (chain == 1) return minw == 6 ? pass_kernel_u<6, false, false, 1, false, false> : pass_kernel_u<5, false, false, 1, false, false>;
     if (chain == 3) return minw == 6 ? pass_kernel_u<6, false, false, 3, false, false> : pass_kernel_u<5, false, false, 3, false, false>;
     if (pf) {  // specialised on the scene's features, or with the tail pool (nullptr: neither applies)
-        PassFnU f = pass_fn_feat(minw, feat);
+        PassFnU f = pass_fn_feat(minw, feat, pool);
         if (f) return f;
     }
     if (pf) return minw == 7 ? pass_kernel_u<7, false, false, 2, true, false>
@@ -1266,7 +1266,7 @@ static bool use_unified(bool leaf1, bool stats, bool qn, int lds_bytes) {
     return leaf1 && !stats && unified_enabled() && lds_bytes <= PT_LDS_TABLES;
 }
 
-bool regroup_applies(bool leaf1, bool stats, bool qn, bool wide, int lds_bytes) {
+static bool regroup_applies(bool leaf1, bool stats, bool qn, bool wide, int lds_bytes) {
     return use_unified(leaf1, stats, qn, lds_bytes) && !qn && !wide;
 }
 
@@ -1290,10 +1290,11 @@ static RgKernel pass_fn_r(int feat) {
     }
 }
 
-hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, bool wide, int feat, bool regroup,
-                       int first_pass, int batch_log2, int write_u8, int grid, bool stats, int lds_bytes,
-                       hipStream_t stream) {
-    if (regroup && regroup_applies(leaf1, stats, qn, wide, lds_bytes)) {
+hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int first_pass, int batch_log2,
+                       int write_u8, int grid, int lds_bytes, hipStream_t stream) {
+    const bool leaf1 = pc.leaf1, qn = pc.qn, wide = pc.wide, stats = pc.stats;
+    const int feat = pc.feat;
+    if (pc.regroup && regroup_applies(leaf1, stats, qn, wide, lds_bytes)) {
         // PT_RG_HANDOFF / PT_RG_WALK_MIN: a walker wave hands its ready paths over once this many are
         // ready or at most this many lanes still walk; PT_RG_BATCH / PT_RG_SPIN: a shader wave shades
         // once this many paths wait, or after this many idle rounds with fewer
@@ -1324,13 +1325,12 @@ hipError_t launch_pass(const LaunchParams* params_dev, bool leaf1, bool qn, bool
         // PT_TAIL_SHADE_MIN / PT_TAIL_WALK_MIN: the shading thresholds of a wave once the work is drained
         static const int tail_shade = env_int("PT_TAIL_SHADE_MIN", shade_min, 1, 64);
         static const int tail_walk = env_int("PT_TAIL_WALK_MIN", walk_min, 0, 64);
-        // PT_TAIL_POOL: a drained wave holding at most this many paths hands them to wave 0 of its
-        // workgroup (pass_kernel_u's tail pool; 0 = off)
-        static const int tail_pool = env_int("PT_TAIL_POOL", 0, 0, 64);
+        const int tail_pool = pc.tail_pool < 0 ? 0 : (pc.tail_pool > 64 ? 64 : pc.tail_pool);
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
             a8 = walk_min, a9 = tail_shade | (tail_walk << 8) | (tail_pool << 16);
         void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8, &a9};
-        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true, feat), qn, wide && !qn, feat), dim3(grid), dim3(PT_UBLOCK), args,
+        hipError_t e = hipLaunchKernel((const void*)pass_fn_u(pass_min_waves(true, feat), qn, wide && !qn, feat, tail_pool),
+                                       dim3(grid), dim3(PT_UBLOCK), args,
                                        (size_t)lds_bytes, stream);
         if (e != hipSuccess) return e;
         return hipGetLastError();
@@ -1362,9 +1362,11 @@ hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256
 }
 
 // The pass kernel launch_pass picks for these arguments, as text (bench.py's roofline.kernel).
-std::string pass_kernel_desc(bool leaf1, bool stats, bool qn, bool wide, int feat, bool regroup, int lds_bytes) {
+std::string pass_kernel_desc(const PassChoice& pc, int lds_bytes) {
+    const bool leaf1 = pc.leaf1, qn = pc.qn, wide = pc.wide, stats = pc.stats;
+    const int feat = pc.feat;
     char buf[160];
-    if (regroup && regroup_applies(leaf1, stats, qn, wide, lds_bytes)) {
+    if (pc.regroup && regroup_applies(leaf1, stats, qn, wide, lds_bytes)) {
         static const int split = env_int("PT_RG_WAVES", 52, 11, 99);
         const int s = (split == 31 || split == 61 || split == 43 || split == 21) ? split : 52;
         std::snprintf(buf, sizeof(buf), "pass_kernel_r<MINW=%d,NWALK=%d,NSHADE=%d,FEAT=%d>", feat == 0 ? 7 : 6, s / 10,
@@ -1373,13 +1375,14 @@ std::string pass_kernel_desc(bool leaf1, bool stats, bool qn, bool wide, int fea
         static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
         static const int chain = env_int("PT_WALK_CHAIN", 2, 1, 3);
         static const int pf = env_int("PT_TRI_PREFETCH", 1, 0, 1);
-        static const int pool = env_int("PT_TAIL_POOL", 0, 0, 64);
+        const int pool = pc.tail_pool;
         int minw = pass_min_waves(true, feat);
         // the instance pass_fn_u picks for this wave target (not every variant has every target)
         if (qn || (chain != 2 && !wide) || (!pf && !wide)) minw = minw == 6 ? 6 : 5;
         else if (wide) minw = minw == 5 ? 5 : 6;
-        const int f = spec && !qn && !wide && pf && chain == 2 ? feat : PT_FEAT_ALL;
-        const bool tp = pool && !qn && !wide && pf && chain == 2 && ((minw == 7 && f == 0) || (minw == 6 && f == PT_FEAT_ALL));
+        int f = spec && !qn && !wide && pf && chain == 2 ? feat : PT_FEAT_ALL;
+        const bool tp = pool > 0 && !qn && !wide && pf && chain == 2;
+        if (tp && !(minw == 7 && f == 0)) { minw = 6; f = PT_FEAT_ALL; }  // pass_fn_feat's tail-pool instances
         std::snprintf(buf, sizeof(buf), "pass_kernel_u<MINW=%d,QN=%d,CHAIN=%d,PF=%d,WIDE=%d,FEAT=%d%s>", minw,
                       qn ? 1 : 0, qn ? 1 : chain, qn ? 0 : pf, wide && !qn ? 1 : 0, f, tp ? ",TAILPOOL" : "");
     } else {
@@ -1389,7 +1392,9 @@ std::string pass_kernel_desc(bool leaf1, bool stats, bool qn, bool wide, int fea
     return buf;
 }
 
-int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int feat, bool regroup, int lds_bytes) {
+int pass_grid_size(const PassChoice& pc, int lds_bytes) {
+    const bool leaf1 = pc.leaf1, qn = pc.qn, wide = pc.wide, stats = pc.stats, regroup = pc.regroup;
+    const int feat = pc.feat;
     int dev = 0, cus = 0, blocks = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1402,7 +1407,7 @@ int pass_grid_size(bool leaf1, bool stats, bool qn, bool wide, int feat, bool re
         return cus * blocks;
     }
     const bool u = use_unified(leaf1, stats, qn, lds_bytes);
-    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true, feat), qn, wide && !qn, feat)
+    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true, feat), qn, wide && !qn, feat, pc.tail_pool)
                        : (const void*)pass_fn(leaf1, stats, pass_min_waves(false, feat), qn);
     const size_t lds = u ? (size_t)lds_bytes : 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, u ? PT_UBLOCK : PT_BLOCK, lds) != hipSuccess || blocks <= 0) blocks = u ? 4 * PT_BLOCK / PT_UBLOCK : 4;

@@ -508,6 +508,7 @@ struct pt_context {
     int wide_mode = -1; // pass_kernel_u walks the wide records: 1 on, 0 off, -1 environment default (PT_WIDE)
     int regroup_mode = -1;  // pass_kernel_r (walker and shader waves): 1 on, 0 off, -1 environment default (PT_REGROUP)
     int grid_share = 100;   // pt_set_grid_share: percent of the occupancy-sized grid a pass launch takes
+    int tail_pool = -1;     // pt_set_tail_pool: pass_kernel_u's tail pool threshold; 0 off, -1 PT_TAIL_POOL
     // pt_set_band_order / pt_band_cost: the order in which this context's bands are handed out, and
     // per-band ray-segment counters (allocated while measuring); both for the current tiling only
     int* band_order = nullptr;
@@ -516,7 +517,7 @@ struct pt_context {
     unsigned int* band_cost = nullptr;
     int band_cost_n = 0;
     bool band_cost_on = false;
-    int grid[2][2][4][4] = {};
+    int grid[2][2][5][4] = {};
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
     size_t ev_used = 0;
@@ -774,11 +775,26 @@ int render_feat(const pt_context* ctx, const DevConfig& dc) {
     return f;
 }
 
+// The pass kernel a render of this context launches (pt_kernels.h PassChoice).
+PassChoice pass_choice(const pt_context* ctx, int feat) {
+    static const int env_pool = env_int("PT_TAIL_POOL", 0, 0, 64);
+    PassChoice pc;
+    pc.leaf1 = ctx->scene.leaf_size == 1;
+    pc.stats = ctx->instrumented;
+    pc.qn = use_qnodes(ctx);
+    pc.wide = use_wide(ctx);
+    pc.feat = feat;
+    pc.regroup = use_regroup(ctx);
+    pc.tail_pool = ctx->tail_pool >= 0 ? ctx->tail_pool : env_pool;
+    return pc;
+}
+
 int pass_grid(pt_context* ctx, int feat) {
-    const bool leaf1 = ctx->scene.leaf_size == 1, qn = use_qnodes(ctx), wide = use_wide(ctx), rg = use_regroup(ctx);
-    int& g = ctx->grid[leaf1 ? 1 : 0][ctx->instrumented ? 1 : 0][qn ? 1 : (wide ? 2 : (rg ? 3 : 0))][feat & 3];
+    const PassChoice pc = pass_choice(ctx, feat);
+    const int variant = pc.qn ? 1 : (pc.wide ? 2 : (pc.regroup ? 3 : (pc.tail_pool > 0 ? 4 : 0)));
+    int& g = ctx->grid[pc.leaf1 ? 1 : 0][pc.stats ? 1 : 0][variant][feat & 3];
     if (g == 0) {
-        g = pass_grid_size(leaf1, ctx->instrumented, qn, wide, feat, rg, pass_lds_bytes(ctx));
+        g = pass_grid_size(pc, pass_lds_bytes(ctx));
         // PT_GRID_PCT: experiment knob, a percentage of the occupancy-sized grid
         const char* e = getenv("PT_GRID_PCT");
         const int pct = e ? atoi(e) : 100;
@@ -938,8 +954,8 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     // a power of two so a unit splits into (pixel, pass) by shift and mask.
     const int feat = render_feat(ctx, dc);
     const int grid = pass_grid(ctx, feat);
-    ctx->last_kernel = pass_kernel_desc(ctx->scene.leaf_size == 1, ctx->instrumented, use_qnodes(ctx), use_wide(ctx),
-                                        feat, use_regroup(ctx), pass_lds_bytes(ctx));
+    const PassChoice pc = pass_choice(ctx, feat);
+    ctx->last_kernel = pass_kernel_desc(pc, pass_lds_bytes(ctx));
     const int units = ctx->tiling.unit_count;
     int most = 1;
     while (most * 2 <= max_pass_batch() && (long long)units * most * 2 <= (1ll << 28)) most *= 2;
@@ -965,9 +981,7 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
         int rc = ev_begin(ctx, 0);
         if (rc != PT_OK) return rc;
-        PT_HIP(launch_pass(ctx->params, ctx->scene.leaf_size == 1, use_qnodes(ctx), use_wide(ctx), feat, use_regroup(ctx),
-                           first, lg, w8, g,
-                           ctx->instrumented, pass_lds_bytes(ctx), ctx->stream));
+        PT_HIP(launch_pass(ctx->params, pc, first, lg, w8, g, pass_lds_bytes(ctx), ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         if (lg > 0) {
             if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;
@@ -1106,6 +1120,12 @@ extern "C" int pt_set_wide_walk(pt_context* ctx, int mode) {
 extern "C" int pt_set_grid_share(pt_context* ctx, int percent) {
     if (!ctx || percent < 1 || percent > 100) { set_error("bad grid share"); return PT_E_ARG; }
     ctx->grid_share = percent;
+    return PT_OK;
+}
+
+extern "C" int pt_set_tail_pool(pt_context* ctx, int paths) {
+    if (!ctx || paths < -1 || paths > 64) { set_error("bad tail pool threshold"); return PT_E_ARG; }
+    ctx->tail_pool = paths;
     return PT_OK;
 }
 

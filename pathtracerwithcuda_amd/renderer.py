@@ -98,6 +98,11 @@ class Renderer:
         """Percentage of the occupancy-sized grid this context's pass launches take (frames in flight)."""
         check(self._lib.pt_set_grid_share(self._ctx, int(percent)), "pt_set_grid_share")
 
+    def set_tail_pool(self, paths: int | None) -> None:
+        """pass_kernel_u's tail pool: a drained wave holding at most `paths` paths hands them to wave 0 of its
+        workgroup (0: off; None: PT_TAIL_POOL). The image is the same either way."""
+        check(self._lib.pt_set_tail_pool(self._ctx, -1 if paths is None else int(paths)), "pt_set_tail_pool")
+
     def band_count(self) -> tuple[int, bool]:
         """(bands of this context's share under its tiling, whether the last one is partial)."""
         n, p = C.c_int(), C.c_int()

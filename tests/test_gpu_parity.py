@@ -35,12 +35,13 @@ def assert_bitwise(gpu, ref, what=""):
                              f"max |d| {np.nanmax(d):.3g}, mean |d| {np.nanmean(d):.3g}")
 
 
-@pytest.fixture(scope="module", params=["persistent", "persistent_wide", "persistent_regroup", "wavefront"])
+@pytest.fixture(scope="module", params=["persistent", "persistent_wide", "persistent_regroup", "persistent_tailpool",
+                                        "wavefront"])
 def gpu(require_gpu, request):
     """Every parity test runs under both kernel schedules (pt_set_schedule), and the persistent one both
     with its default walk (the binary nodes) and walking the wide BVH records where the scene has them
-    (pt_set_wide_walk, pt_path.h walk_wide) and as walker and shader waves (pt_set_regroup,
-    pass_kernel_r): they must all agree bitwise."""
+    (pt_set_wide_walk, pt_path.h walk_wide), as walker and shader waves (pt_set_regroup,
+    pass_kernel_r) and with the tail pool (pt_set_tail_pool): they must all agree bitwise."""
     r = pt.Renderer(0)
     sched = "wavefront" if request.param == "wavefront" else "persistent"
     r.set_schedule(sched)
@@ -49,6 +50,8 @@ def gpu(require_gpu, request):
         r.set_wide_walk(True)
     if request.param == "persistent_regroup":
         r.set_regroup(True)
+    if request.param == "persistent_tailpool":
+        r.set_tail_pool(32)
     yield r
     r.close()
 
@@ -322,11 +325,13 @@ def test_c5_4k_textured_depth12_frame(bench_gpu):
     assert launches == {0: 1, 3: 1}, launches
 
 
+@pytest.mark.parametrize("variant", ["regroup", "tailpool"])
 @pytest.mark.parametrize("workload", ["metric", "c4", "c5"])
-def test_regrouped_waves_at_the_bench_launch_shape(bench_gpu, c4_workload, workload):
-    """pass_kernel_r (walker waves and shader waves exchanging paths through LDS) on the bench's launch
-    shape and the C4/C5 configurations: bit-identical to the oracle on a pixel subset and to pass_kernel_u
-    on the whole frame, the same ray-segment count, and no wave gave up waiting (stats[15])."""
+def test_alternative_kernels_at_the_bench_launch_shape(bench_gpu, c4_workload, workload, variant):
+    """pass_kernel_r (walker waves and shader waves exchanging paths through LDS) and pass_kernel_u with the
+    tail pool, on the bench's launch shape and the C4/C5 configurations: bit-identical to the oracle on a
+    pixel subset and to the default kernel on the whole frame, the same ray-segment count, and no
+    pass_kernel_r wave gave up waiting (stats[15])."""
     import bench
     wl = c4_workload if workload == "c4" else bench.Workload(workload)
     r = bench_gpu
@@ -337,11 +342,17 @@ def test_regrouped_waves_at_the_bench_launch_shape(bench_gpu, c4_workload, workl
     r.synchronize()
     base, base8 = r.download()
     base_segments = r.stats()["segments"]
-    assert r.last_kernel().startswith("pass_kernel_u")
-    r.set_regroup(True)
+    assert r.last_kernel().startswith("pass_kernel_u") and "TAILPOOL" not in r.last_kernel()
+    if variant == "regroup":
+        r.set_regroup(True)
+    else:
+        r.set_tail_pool(32)
     try:
         launches, img = _render_workload_subset(r, wl, passes=8, npx=10000, seed=3)
-        assert r.last_kernel().startswith("pass_kernel_r"), r.last_kernel()
+        if variant == "regroup":
+            assert r.last_kernel().startswith("pass_kernel_r"), r.last_kernel()
+        else:
+            assert "TAILPOOL" in r.last_kernel(), r.last_kernel()
         raw = r.stats_raw()
         assert raw[15] == 0, "a pass_kernel_r wave gave up waiting"
         assert raw[0] == base_segments
@@ -349,6 +360,7 @@ def test_regrouped_waves_at_the_bench_launch_shape(bench_gpu, c4_workload, workl
         img8 = r.download()[1]
     finally:
         r.set_regroup(None)
+        r.set_tail_pool(None)
     assert np.array_equal(img, base)
     assert np.array_equal(img8, base8)
 
