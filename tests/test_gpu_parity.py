@@ -560,7 +560,8 @@ def test_edge_cases(gpu, case):
 @pytest.mark.parametrize("inflight", [2, 3])
 def test_frames_in_flight_equal_one_at_a_time(require_gpu, inflight):
     """bench.py's frame pipeline: frames queued on several contexts with no host sync between them
-    (TiledFrame.launch) each end with the image of a frame rendered on its own, bit for bit."""
+    (TiledFrame.launch) each end with the image of a frame rendered on its own, bit for bit; with three
+    contexts each launches on half the grid and the last frame on the whole grid, as bench.py does."""
     sc = pt.cornell_scene(pt.torus_knot(80, 24), cube_length=32)
     cfg = pt.configuration(max_tracer_depth=8)
     cam = pt.camera(96, 64, **BENCH_CAM)
@@ -570,8 +571,13 @@ def test_frames_in_flight_equal_one_at_a_time(require_gpu, inflight):
         frames = []
         for q in rs:
             q.upload(sc, cfg)
+            if inflight >= 3:
+                q.set_grid_share(50)
             frames.append(pt.TiledFrame(q, 96, 64))
-        for i in range(2 * inflight + 1):
+        n = 2 * inflight + 1
+        for i in range(n):
+            if inflight >= 3 and i == n - 1:
+                rs[i % inflight].set_grid_share(100)
             frames[i % inflight].launch(cam, cfg, 4)
         for f in frames:
             f.synchronize()
