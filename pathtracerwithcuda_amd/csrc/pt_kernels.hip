@@ -693,6 +693,7 @@ __global__ __launch_bounds__((NWALK + NSHADE) * 64, MINW) void pass_kernel_r(
     const float clamp_hi = (float)P0->cfg.max_depth * 2.0f;
     const unsigned long long below = lanes_below(lane);
     __shared__ int2 lds_mesh[PT_LDS_MESHES];
+    __shared__ int4 lds_next[PT_LDS_MESHES + 1];
     __shared__ float4 slot_q[5][S];
     __shared__ int slot_state[S];
     __shared__ int scratch[NWALK + NSHADE][128];
@@ -712,6 +713,14 @@ __global__ __launch_bounds__((NWALK + NSHADE) * 64, MINW) void pass_kernel_r(
         for (int i = threadIdx.x; i < S; i += NT) slot_state[i] = SLOT_FREE;
         if (threadIdx.x == 0) walkers_done = 0;
         __syncthreads();
+        if (uniform_int(P0->sc.mesh_num) <= PT_LDS_MESHES) {  // lds_next (start_mesh_next)
+            for (int i = threadIdx.x; i <= n; i += NT) {
+                int j = i;
+                while (j < n && lds_mesh[j].x == lds_mesh[j].y) j++;
+                lds_next[i] = j < n ? make_int4(lds_mesh[j].x, lds_mesh[j].y, j, 0) : make_int4(0, 0, n, 0);
+            }
+            __syncthreads();
+        }
     }
     const float4* lds_spheres = lds_dyn + uniform_int(P0->sc.material_num) * (int)(sizeof(DevMaterial) / 16);
     float4* const q[5] = {slot_q[0], slot_q[1], slot_q[2], slot_q[3], slot_q[4]};
@@ -836,7 +845,9 @@ __global__ __launch_bounds__((NWALK + NSHADE) * 64, MINW) void pass_kernel_r(
                     h.t = w.t; h.t1 = w.t1; h.t2 = w.t2; h.prim = w.tri; h.type = 2;
                 }
                 mesh++;
-                mode = start_mesh(sc, lds_mesh, nullptr, false, mesh, w) ? LANE_WALK : LANE_READY;
+                const bool more = sc.mesh_num <= PT_LDS_MESHES ? start_mesh_next(lds_next, mesh, w)
+                                                               : start_mesh(sc, lds_mesh, nullptr, false, mesh, w);
+                mode = more ? LANE_WALK : LANE_READY;
             };
             float4 pta = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ptb = pta, ptc = pta;
             for (int k = 0; k < walk_steps; k++) {
