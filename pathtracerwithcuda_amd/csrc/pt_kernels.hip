@@ -36,6 +36,10 @@ namespace pt {
 #ifndef PT_NEXT_MESH
 #define PT_NEXT_MESH 1
 #endif
+// PT_ROOT_SKIP: segments test every mesh's root box at their start and skip the meshes they miss
+#ifndef PT_ROOT_SKIP
+#define PT_ROOT_SKIP 1
+#endif
 template <class T>
 __device__ __forceinline__ void opaque(T& x) {
     int* p = reinterpret_cast<int*>(&x);
@@ -262,6 +266,56 @@ __device__ __forceinline__ int begin_segment(const DevScene& sc, const int2* lds
     return LANE_WALK;
 }
 
+// ---- root boxes at segment start (pass_kernel_u, binary walk, at most PT_ROOT_MESHES meshes) ----------
+// Each mesh's walk starts at its root with a local min_t of infinity (intersect_triangle_mesh_bvh,
+// :113-150), so a ray whose slab test fails on a mesh's root box gets nothing from that mesh. The roots of
+// the first PT_ROOT_MESHES meshes are kept in LDS; a segment tests them all at its start and walks only the
+// meshes whose root passes, starting below a passing internal root (the test there would repeat the same
+// test with the same infinite min_t). `mesh` then holds the mesh being walked in bits 0-7 and the meshes
+// still to walk as a bit mask from bit 8 on (bit 8 + i: mesh i), so the skip costs no register.
+#define PT_ROOT_MESHES 24
+__device__ __forceinline__ void root_walk_start(const int2* lds_mesh, const float4* lds_root, int m, MeshWalk& w) {
+    const int2 r = lds_mesh[m];
+    w.pos = f2i(lds_root[2 * m + 1].w) < 0 ? r.x + 1 : r.x;  // below an internal root, at a leaf root
+    w.end = r.y;
+    w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
+}
+__device__ __forceinline__ int begin_segment_roots(const DevScene& sc, const int2* lds_mesh, const float4* lds_root,
+                                                   const PathState& ps, v3& inv, Hit& h, MeshWalk& w, int& mesh) {
+    h.t = __builtin_inff(); h.t1 = __builtin_inff(); h.t2 = __builtin_inff();
+    h.type = 0; h.prim = -1;
+    for (int i = 0; i < sc.sphere_num; i++) {
+        float t;
+        if (sphere_t(sc.spheres[2 * i], ps.o, ps.d, &t) && t < h.t && t > 0.0f) {
+            h.t = t; h.prim = i; h.type = 1;
+        }
+    }
+    if (sc.first_mesh >= sc.mesh_num) return LANE_READY;
+    inv = mk3(rcp_exact(ps.d.x), rcp_exact(ps.d.y), rcp_exact(ps.d.z));  // == 1.0f / d
+    unsigned int todo = 0;
+    for (int i = sc.first_mesh; i < sc.mesh_num; i++) {  // wave-uniform loop, broadcast LDS reads
+        const int2 r = lds_mesh[i];
+        if (r.x == r.y) continue;
+        float entry;
+        if (box_hit(lds_root[2 * i], lds_root[2 * i + 1], ps.o, inv, &entry) && entry <= __builtin_inff())
+            todo |= 1u << i;
+    }
+    if (!todo) return LANE_READY;
+    const int m = __builtin_ctz(todo);
+    mesh = m | (int)((todo & (todo - 1u)) << 8);
+    root_walk_start(lds_mesh, lds_root, m, w);
+    return LANE_WALK;
+}
+// The next mesh of a root-masked segment (mesh_done): false when none is left.
+__device__ __forceinline__ bool next_root_mesh(const int2* lds_mesh, const float4* lds_root, int& mesh, MeshWalk& w) {
+    const unsigned int rest = (unsigned int)mesh >> 8;
+    if (!rest) return false;
+    const int m = __builtin_ctz(rest);
+    mesh = m | (int)((rest & (rest - 1u)) << 8);
+    root_walk_start(lds_mesh, lds_root, m, w);
+    return true;
+}
+
 // pixel_256_transform_gamma_corrected_kernel (:644-680) for one finished (pixel, pass) unit
 // depth: the path's ray segments, counted into its band when the context measures band costs.
 __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfig& cfg, const DevOutput& out,
@@ -332,6 +386,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     __shared__ int2 lds_mesh[PT_LDS_MESHES];
     __shared__ int lds_wroot[WIDE ? PT_LDS_MESHES : 1];
     __shared__ int4 lds_next[PT_LDS_MESHES + 1];
+    __shared__ float4 lds_root[2 * PT_ROOT_MESHES];
     __shared__ float4 tp_q[4][TP ? PT_TP_SLOTS : 1];
     __shared__ int tp_state[TP ? PT_TP_SLOTS : 1];        // 0 free, 1 full
     __shared__ int tp_scr[PT_UBLOCK / 64][TP ? PT_TP_SLOTS : 1];
@@ -364,6 +419,13 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 int j = i;
                 while (j < n && lds_mesh[j].x == lds_mesh[j].y) j++;
                 lds_next[i] = j < n ? make_int4(lds_mesh[j].x, lds_mesh[j].y, j, 0) : make_int4(0, 0, n, 0);
+            }
+            if (!WIDE && PT_ROOT_SKIP && n <= PT_ROOT_MESHES) {  // lds_root (begin_segment_roots)
+                const float4* nodes = uniform_ptr(P0->sc.nodes);
+                for (int i = threadIdx.x; i < 2 * n; i += PT_UBLOCK) {
+                    const int2 r = lds_mesh[i >> 1];
+                    lds_root[i] = r.x != r.y ? nodes[2 * r.x + (i & 1)] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                }
             }
             __syncthreads();
         }
@@ -398,6 +460,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         const DevConfig cfg = load_const(&P->cfg);
         const DevTiling til = load_const(&P->til);
         const DevOutput out = load_const(&P->out);
+        const bool roots = !WIDE && !QN && PT_ROOT_SKIP && sc.mesh_num <= PT_ROOT_MESHES;  // wave-uniform
         if (PROF) { prof[0]++; tc = __builtin_readcyclecounter(); }
 
         // lanes without a path take the next (pixel, pass) units, one atomic per wave (pt_work.h)
@@ -494,7 +557,10 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 }
             }
         }
-        if (mode == LANE_NEW) mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
+        if (mode == LANE_NEW) {
+            if (roots) mode = begin_segment_roots(sc, lds_mesh, lds_root, ps, inv, h, w, mesh);
+            else mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
+        }
         if (!__any(mode != LANE_DONE)) break;
         if (PROF) { const unsigned long long t = __builtin_readcyclecounter(); prof[8] += t - tc; tc = t; }
 
@@ -548,10 +614,14 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (w.tri >= 0 && w.t < h.t) {
                 h.t = w.t; h.t1 = w.t1; h.t2 = w.t2; h.prim = w.tri; h.type = 2;
             }
-            mesh++;
             bool more;
-            if (PT_NEXT_MESH && !WIDE && sc.mesh_num <= PT_LDS_MESHES) more = start_mesh_next(lds_next, mesh, w);
-            else more = start_mesh(sc, lds_mesh, lds_wroot, WIDE && w.end < 0, mesh, w);
+            if (roots) {
+                more = next_root_mesh(lds_mesh, lds_root, mesh, w);
+            } else {
+                mesh++;
+                if (PT_NEXT_MESH && !WIDE && sc.mesh_num <= PT_LDS_MESHES) more = start_mesh_next(lds_next, mesh, w);
+                else more = start_mesh(sc, lds_mesh, lds_wroot, WIDE && w.end < 0, mesh, w);
+            }
             mode = more ? LANE_WALK : LANE_READY;
         };
         // PF: the parked triangle's geometry, loaded at the park; scoped to the walk loop, which no lane
