@@ -37,6 +37,9 @@ namespace pt {
 #define PT_NEXT_MESH 1
 #endif
 // PT_ROOT_SKIP: segments test every mesh's root box at their start and skip the meshes they miss
+#ifndef PT_PROF_MESH
+#define PT_PROF_MESH 0
+#endif
 #ifndef PT_ROOT_SKIP
 #define PT_ROOT_SKIP 1
 #endif
@@ -632,9 +635,15 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (PROF) {
                 prof[1]++; prof[2] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK));
                 prof[12] += (unsigned long long)__popcll(__ballot(mode == LANE_TRI));
+#if PT_PROF_MESH  // diagnostic builds: walking lanes per mesh (meshes 0, 1, 2) instead of the drained/ready/idle counts
+                prof[11] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK && (mesh & 0xff) == 0));
+                prof[13] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK && (mesh & 0xff) == 1));
+                prof[14] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK && (mesh & 0xff) == 2));
+#else
                 if (drained) prof[11] += 1ull | ((unsigned long long)__popcll(__ballot(mode == LANE_WALK)) << 32);
                 prof[13] += (unsigned long long)__popcll(__ballot(mode == LANE_READY));
                 prof[14] += (unsigned long long)__popcll(__ballot(mode == LANE_WANT || mode == LANE_DONE));
+#endif
             }
             if (mode == LANE_WALK) {
                 if (PT_DUP == 2) {
