@@ -1390,7 +1390,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
         // once this many paths wait, or after this many idle rounds with fewer
         static const int chunk = env_int("PT_CHUNK_MEGA", 64, 0, 4096);
         static const int handoff = env_int("PT_RG_HANDOFF", 16, 1, 64);
-        static const int walk_steps = env_int("PT_WALK_STEPS", 10, 1, 64);
+        static const int walk_steps = env_int("PT_WALK_STEPS", 8, 1, 64);
         static const int tri_min = env_int("PT_TRI_MIN", 6, 1, 64);
         static const int walk_min = env_int("PT_RG_WALK_MIN", 40, 0, 64);
         static const int batch = env_int("PT_RG_BATCH", 48, 1, 64);
@@ -1408,7 +1408,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
         // 64-unit chunks and a 28-lane shading batch: measured best with frames in flight
         static const int chunk = env_int("PT_CHUNK_MEGA", 64, 0, 4096);
         static const int shade_min = env_int("PT_SHADE_MIN", 28, 1, 64);
-        static const int walk_steps = env_int("PT_WALK_STEPS", 10, 1, 64);
+        static const int walk_steps = env_int("PT_WALK_STEPS", 8, 1, 64);
         const LaunchParams* a0 = params_dev;
         static const int tri_min = env_int("PT_TRI_MIN", 6, 1, 64);  // measured best with frames in flight
         static const int walk_min = env_int("PT_WALK_MIN", 8, 0, 64);
