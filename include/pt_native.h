@@ -107,7 +107,8 @@ void* pt_image256_device_ptr(pt_context* ctx);
 int pt_stats_reset(pt_context* ctx);
 int pt_stats(pt_context* ctx, unsigned long long* segments, unsigned long long* nodes, unsigned long long* tris);
 /* All counters: [0] segments, [1] nodes, [2] triangle tests, [3] mesh hits, [4] sphere hits,
- * [5] misses, [6] subsurface scatter events ([1..6] instrumented kernel only). n <= 32. */
+ * [5] misses, [6] subsurface scatter events ([1..6] instrumented kernel only); [16..47] the
+ * PT_UPROF build's profile counters (tools/uprof.py). n <= 64. */
 int pt_stats_all(pt_context* ctx, unsigned long long* out, int n);
 int pt_set_instrumented(pt_context* ctx, int on);
 /* Kernel schedule of a pass (results are bit-identical under both):

@@ -453,6 +453,10 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     bool drained = false;
     unsigned long long prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tc = 0, tc2 = 0;
+    // PROF timeline (stats[32..40]): this wave's start, the refill that first found the work drained,
+    // its end (real-time clock), and the paths it shaded after the drain
+    unsigned long long t_start = 0, t_drain = 0, tail_segments = 0;
+    if (PROF) t_start = __builtin_amdgcn_s_memrealtime();
     while (true) {
         const LaunchParams* P = params;
         asm volatile("" : "+s"(P));
@@ -473,6 +477,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             const unsigned int u = work_take(out.fetch, regions.stride, regions, (unsigned int)chunk, need_mask, want,
                                              lanes_below(lane), cursor, drained);
             if (PROF) prof[7] += (unsigned long long)__popcll(__ballot(want && u != ~0u));
+            if (PROF && drained && t_drain == 0) t_drain = __builtin_amdgcn_s_memrealtime();
             if (want) {
                 if (u != ~0u) {
                     unit = u;
@@ -575,6 +580,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         const unsigned int wmin = drained ? (unsigned int)(tail >> 8) : (unsigned int)walk_min;
         if (ready && (__popcll(walking) <= wmin || __popcll(ready) >= smin)) {
             if (PROF) { prof[3]++; prof[4] += (unsigned long long)__popcll(ready); }
+            if (PROF && drained) tail_segments += (unsigned long long)__popcll(ready);
             segments += (unsigned long long)__popcll(ready);
             bool alive = false;
             if (mode == LANE_READY) {
@@ -705,6 +711,15 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         if (PROF) {
 #pragma unroll
             for (int k = 0; k < 16; k++) atomicAdd(&P0->out.stats[16 + k], prof[k]);
+            // minima as maxima of the complement, so a zeroed buffer starts every slot
+            const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+            if (t_drain == 0) t_drain = t_end;
+            unsigned long long* tl = P0->out.stats + 32;
+            atomicMax(&tl[0], ~t_start); atomicMax(&tl[1], t_start);
+            atomicMax(&tl[2], ~t_drain); atomicMax(&tl[3], t_drain);
+            atomicMax(&tl[4], ~t_end); atomicMax(&tl[5], t_end);
+            atomicAdd(&tl[6], t_end - t_drain); atomicAdd(&tl[7], t_end - t_start);
+            atomicAdd(&tl[8], 1ull); atomicAdd(&tl[9], tail_segments);
         }
     }
 }

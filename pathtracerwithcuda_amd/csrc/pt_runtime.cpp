@@ -23,6 +23,9 @@
 #include "../../include/pt_native.h"
 #include "pt_kernels.h"
 
+// the context's counter buffer: stats[0..15] (pt_stats_all), [16..47] PT_UPROF profile counters
+#define PT_STATS_BYTES 512
+
 using namespace pt;
 
 namespace {
@@ -1043,9 +1046,9 @@ extern "C" int pt_context_create(int device, pt_context** out) {
     int rc = ensure_device(ctx);
     if (rc == PT_OK && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { set_error("stream"); rc = PT_E_HIP; }
     if (rc == PT_OK && hipMalloc(&ctx->fetch, PT_HEAD_SET * sizeof(unsigned int)) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
-    if (rc == PT_OK && hipMalloc(&ctx->stats, 256) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
+    if (rc == PT_OK && hipMalloc(&ctx->stats, PT_STATS_BYTES) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
     if (rc == PT_OK && hipMalloc(&ctx->params, sizeof(LaunchParams)) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
-    if (rc == PT_OK && hipMemset(ctx->stats, 0, 256) != hipSuccess) { set_error("memset"); rc = PT_E_HIP; }
+    if (rc == PT_OK && hipMemset(ctx->stats, 0, PT_STATS_BYTES) != hipSuccess) { set_error("memset"); rc = PT_E_HIP; }
     if (rc != PT_OK) { pt_context_destroy(ctx); return rc; }
     *out = ctx;
     return PT_OK;
@@ -1344,14 +1347,14 @@ extern "C" int pt_stats_reset(pt_context* ctx) {
     if (!ctx) return PT_E_ARG;
     PT_HIP(hipSetDevice(ctx->device));
     PT_HIP(hipStreamSynchronize(ctx->stream));
-    PT_HIP(hipMemsetAsync(ctx->stats, 0, 256, ctx->stream));
+    PT_HIP(hipMemsetAsync(ctx->stats, 0, PT_STATS_BYTES, ctx->stream));
     PT_HIP(hipStreamSynchronize(ctx->stream));
     ctx->ev_used = 0;
     return PT_OK;
 }
 
 extern "C" int pt_stats_all(pt_context* ctx, unsigned long long* out, int n) {
-    if (!ctx || !out || n < 0 || n > 32) return PT_E_ARG;
+    if (!ctx || !out || n < 0 || n > PT_STATS_BYTES / 8) return PT_E_ARG;
     PT_HIP(hipSetDevice(ctx->device));
     PT_HIP(hipMemcpyAsync(out, ctx->stats, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
     PT_HIP(hipStreamSynchronize(ctx->stream));

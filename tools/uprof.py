@@ -20,13 +20,16 @@ r.setup_frame(bench.WIDTH, bench.HEIGHT)
 TILE = int(os.environ.get("PT_UPROF_TILE", "1"))  # >1: rank 0's bands of an N-way tiled frame
 if TILE > 1:
     r.set_tiling(bench.BAND_ROWS, TILE, 0)
+SHARE = int(os.environ.get("PT_UPROF_SHARE", "100"))  # percent of the occupancy grid (frames in flight)
+if SHARE != 100:
+    r.set_grid_share(SHARE)
 r.render(cam, cfg, 1, bench.SPP, write_u8=2)
 r.synchronize()
 r.stats_reset()
 r.render(cam, cfg, 1, bench.SPP, write_u8=2)
 r.synchronize()
-buf = (C.c_ulonglong * 32)()
-pt.lib().pt_stats_all(r._ctx, buf, 32)
+buf = (C.c_ulonglong * 48)()
+pt.lib().pt_stats_all(r._ctx, buf, 48)
 v = list(buf)
 if os.environ.get("PT_REGROUP") == "1":
     names = ["w_rounds", "handoffs", "lanes_handed", "walk_steps", "walking_lanes", "w_idle_rounds", "shade_batches",
@@ -70,4 +73,19 @@ d["drained_walking_lanes"] = d.pop("drained_steps_lanes") >> 32
 d["drained_frac_of_walk_steps"] = round(d["drained_walk_steps"] / max(d["walk_steps"], 1), 3)
 d["drained_lanes_per_walk_step"] = round(d["drained_walking_lanes"] / max(d["drained_walk_steps"], 1), 2)
 d["next_segment_frac_of_shade"] = round(d["cyc_next_segment"] / max(d["cyc_shade"], 1), 3)
+# timeline (stats[32..41], real-time clock at 100 MHz): waves' start, first drained refill, end
+M = (1 << 64) - 1
+tl = v[32:42]
+if tl[8]:
+    t0 = M ^ tl[0]
+    us = lambda t: round((t - t0) / 100.0, 1)  # noqa: E731
+    d["tl_waves"] = tl[8]
+    d["tl_start_last_us"] = us(tl[1])
+    d["tl_drain_first_us"] = us(M ^ tl[2])
+    d["tl_drain_last_us"] = us(tl[3])
+    d["tl_end_first_us"] = us(M ^ tl[4])
+    d["tl_end_last_us"] = us(tl[5])
+    d["tl_wave_tail_avg_us"] = round(tl[6] / tl[8] / 100.0, 1)
+    d["tl_wave_life_avg_us"] = round(tl[7] / tl[8] / 100.0, 1)
+    d["tl_segments_after_drain_frac"] = round(tl[9] / max(d["segments"], 1), 3)
 print(json.dumps(d))
