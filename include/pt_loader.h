@@ -70,6 +70,13 @@ int pt_scene_load(pt_scene_builder* builder, const char* scene_path, const pt_sc
 /* RGBA8, top row first, alpha 255 (FreeImage_ConvertTo24Bits then RGBA). *rgba is malloc'd. */
 int pt_image_load(const char* path, int* width, int* height, unsigned char** rgba);
 void pt_image_free(unsigned char* rgba);
+/* JPEG decoding of pt_image_load with a chosen arithmetic (pt_jpeg.cpp): PT_JPEG_IJG9 is libjpeg 9a's
+ * fast IDCT and colour tables, what FreeImage 3.17 runs by default and what pt_image_load uses;
+ * PT_JPEG_IJG6 is libjpeg 6b's (libjpeg-turbo's), the test hook that pins the shared decoder against
+ * PIL. RGBA8, top row first; free with pt_image_free. */
+#define PT_JPEG_IJG9 0
+#define PT_JPEG_IJG6 1
+int pt_jpeg_decode(const unsigned char* data, size_t size, int variant, int* width, int* height, unsigned char** rgba);
 /* channels 3 (RGB) or 4 (RGBA), top row first. */
 int pt_image_write_png(const char* path, int width, int height, const unsigned char* pixels, int channels);
 

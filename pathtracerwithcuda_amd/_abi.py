@@ -268,6 +268,7 @@ _PROTOS = {
     "pt_scene_load": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(SceneLoadOptions)]),
     "pt_image_load": (C.c_int, [C.c_char_p, c_int_p, c_int_p, C.POINTER(c_ubyte_p)]),
     "pt_image_free": (None, [c_ubyte_p]),
+    "pt_jpeg_decode": (C.c_int, [c_ubyte_p, C.c_size_t, C.c_int, c_int_p, c_int_p, C.POINTER(c_ubyte_p)]),
     "pt_image_write_png": (C.c_int, [C.c_char_p, C.c_int, C.c_int, c_ubyte_p, C.c_int]),
 }
 

@@ -9,7 +9,7 @@
 //   TGA  types 1/2/3 and their RLE forms 9/10/11; 8/15/16/24/32 bpp; either origin
 //   PNG  every colour type and bit depth, Adam7 interlacing (zlib inflate)
 // 16-bit channels keep their high byte and 5/6-bit channels expand as c * 255 / 31 (or 63), as
-// FreeImage's ConvertTo24Bits does. JPEG is not decoded (decoder-dependent pixels).
+// FreeImage's ConvertTo24Bits does. JPEG: pt_jpeg.cpp (libjpeg 9a's fast IDCT, FreeImage's default).
 // The PNG writer stores the 8-bit framebuffer (the reference's screenshot, Main/window.cpp:712-740).
 #include <zlib.h>
 
@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/pt_loader.h"
+#include "pt_jpeg.h"
 
 namespace {
 
@@ -361,7 +362,9 @@ extern "C" int pt_image_load(const char* path, int* width, int* height, unsigned
     static const unsigned char png_sig[4] = {137, 80, 78, 71};
     if (d.size() >= 4 && !std::memcmp(d.data(), png_sig, 4)) ok = decode_png(d, im, err);
     else if (d.size() >= 2 && d[0] == 'B' && d[1] == 'M') ok = decode_bmp(d, im, err);
-    else if (d.size() >= 3 && d[0] == 0xFF && d[1] == 0xD8 && d[2] == 0xFF) { ok = false; err = "JPEG is not supported"; }
+    else if (d.size() >= 3 && d[0] == 0xFF && d[1] == 0xD8 && d[2] == 0xFF) {
+        ok = pt::decode_jpeg(d.data(), d.size(), PT_JPEG_IJG9, &im.w, &im.h, im.rgba, err);
+    }
     else if (lower_ext(path) == "tga") ok = decode_tga(d, im, err);
     else { ok = false; err = "Unsupported image file format"; }
     if (!ok) {

@@ -70,6 +70,24 @@ def load_image(path: str) -> np.ndarray:
         lib().pt_image_free(px)
 
 
+JPEG_IJG9, JPEG_IJG6 = 0, 1  # include/pt_loader.h PT_JPEG_IJG9 / PT_JPEG_IJG6
+
+
+def decode_jpeg(data: bytes, variant: int = JPEG_IJG9) -> np.ndarray:
+    """JPEG bytes -> (H, W, 4) uint8 RGBA with a chosen libjpeg arithmetic (pt_jpeg_decode): JPEG_IJG9 is
+    what load_image uses (FreeImage's libjpeg 9a), JPEG_IJG6 the libjpeg-turbo arithmetic the tests pin."""
+    w, h = C.c_int(), C.c_int()
+    px = _abi.c_ubyte_p()
+    buf = (C.c_ubyte * len(data)).from_buffer_copy(data)
+    rc = lib().pt_jpeg_decode(buf, len(data), variant, C.byref(w), C.byref(h), C.byref(px))
+    if rc != 0:
+        raise _abi.PtError(f"decode_jpeg failed ({rc})")
+    try:
+        return np.ctypeslib.as_array(px, (h.value, w.value, 4)).copy()
+    finally:
+        lib().pt_image_free(px)
+
+
 def write_png(path: str, pixels: np.ndarray) -> None:
     """8-bit RGB or RGBA (H, W, 3|4), top row first, through the C++ writer."""
     pixels = np.ascontiguousarray(pixels, np.uint8)

@@ -741,11 +741,7 @@ def test_reference_scene_files(gpu, tmp_path, name, bvh):
     cfg = pt.load_config(str(root / "res" / "configuration" / "config.json"))
     cfg.bvh_build = bvh
     cfg.max_tracer_depth = 6
-    bg = fmt = None
-    if name == "micro_surface":
-        bg, fmt = "res\\texture\\yokohama", "bmp"
-    sc = pt.load_scene(str(root / "res" / "scene" / f"{name}.json"), root_dir=str(root), config=cfg, background=bg,
-                       background_format=fmt)
+    sc = pt.load_scene(str(root / "res" / "scene" / f"{name}.json"), root_dir=str(root), config=cfg)
     kw = dict(BENCH_CAM) if name.startswith("cornell") else {}
     if name == "depth_of_view":
         kw.update(aperture=0.15, focal=13.0)

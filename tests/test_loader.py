@@ -42,7 +42,8 @@ def write_bmp24(path, rgb):
 
 def make_root(tmp_path, sky=16):
     """A reference-style working directory: res/ from the fixtures plus a generated yokohama skybox
-    (absent from the checkout) and tex_cube texture."""
+    (absent from the checkout), a generated JPEG maskonaive skybox (micro_surface.json; the
+    reference's 2048^2 faces are too large for fixtures) and the tex_cube texture."""
     root = tmp_path / "gpt"
     shutil.copytree(RES, root / "res")
     rng = np.random.default_rng(11)
@@ -50,6 +51,13 @@ def make_root(tmp_path, sky=16):
     sky_dir.mkdir(parents=True)
     for face in ("xpos", "xneg", "ypos", "yneg", "zpos", "zneg"):
         write_bmp24(str(sky_dir / f"{face}.bmp"), rng.integers(0, 256, (sky, sky, 3), dtype=np.uint8))
+    jpg_dir = root / "res" / "texture" / "maskonaive"
+    jpg_dir.mkdir(parents=True)
+    y, x = np.mgrid[0:sky, 0:sky]
+    for i, face in enumerate(("xpos", "xneg", "ypos", "yneg", "zpos", "zneg")):
+        grad = np.stack([x * 255 // sky, y * 255 // sky, np.full_like(x, 40 * i)], -1)
+        img = np.clip(grad + rng.integers(-30, 31, grad.shape), 0, 255).astype(np.uint8)
+        PIL.fromarray(img, "RGB").save(str(jpg_dir / f"{face}.jpg"), quality=85, subsampling=2)  # 4:2:0 as theirs
     tex_dir = root / "res" / "texture" / "tex_cube"
     tex_dir.mkdir(parents=True)
     PIL.fromarray(rng.integers(0, 256, (24, 40, 4), dtype=np.uint8), "RGBA").save(str(tex_dir / "uv.png"))
@@ -235,9 +243,9 @@ def test_png_writer_round_trip(tmp_path):
 def test_unsupported_or_missing_images_fail_loudly(tmp_path):
     with pytest.raises(pt.PtError):
         pt.load_image(str(tmp_path / "nope.bmp"))
-    p = tmp_path / "x.jpg"
+    p = tmp_path / "x.gif"
     PIL.fromarray(np.zeros((8, 8, 3), np.uint8)).save(str(p))
-    with pytest.raises(pt.PtError):  # JPEG is outside the decoded formats
+    with pytest.raises(pt.PtError):  # GIF is outside the decoded formats (unsupported JPEGs: test_jpeg.py)
         pt.load_image(str(p))
 
 
@@ -277,11 +285,12 @@ def test_cornell_json_equals_the_programmatic_scene(tmp_path):
                                   "refractive_index", "tex_cube"])
 def test_reference_scene_files_load(tmp_path, name):
     root = make_root(tmp_path)
-    bg = fmt = None
-    if name == "micro_surface":  # its maskonaive skybox is JPEG: use the BMP stand-in
-        bg, fmt = "res\\texture\\yokohama", "bmp"
-    sc = pt.load_scene(str(root / "res" / "scene" / f"{name}.json"), root_dir=str(root), background=bg,
-                       background_format=fmt)
+    sc = pt.load_scene(str(root / "res" / "scene" / f"{name}.json"), root_dir=str(root))
+    if name == "micro_surface":  # its maskonaive skybox is JPEG, decoded as libjpeg 9a (test_jpeg.py)
+        cm = sc.view.sky_cube_map.contents
+        px = np.ctypeslib.as_array(cm.m_y_negative_map, (16 * 16 * 4,)).reshape(16, 16, 4)
+        face = open(str(root / "res" / "texture" / "maskonaive" / "yneg.jpg"), "rb").read()
+        assert cm.length == 16 and np.array_equal(px, pt.loader.decode_jpeg(face))
     spec = json.load(open(os.path.join(RES, "scene", f"{name}.json")))
     assert sc.view.sphere_num == len(spec.get("Sphere", []))
     assert sc.view.mesh_num == len(spec.get("Mesh", []))

@@ -79,7 +79,11 @@ def _images(d):
                           ("rgb.bmp", PIL.fromarray(rgb, "RGB"), {}),
                           ("pal.bmp", PIL.fromarray(rgb, "RGB").quantize(16), {}),
                           ("rgb.tga", PIL.fromarray(rgb, "RGB"), {}),
-                          ("rgba_rle.tga", PIL.fromarray(rgba, "RGBA"), {"compression": "tga_rle"})):
+                          ("rgba_rle.tga", PIL.fromarray(rgba, "RGBA"), {"compression": "tga_rle"}),
+                          ("rgb420.jpg", PIL.fromarray(rgb, "RGB"), {"quality": 80, "subsampling": 2}),
+                          ("rgb444_rst.jpg", PIL.fromarray(rgb, "RGB"),
+                           {"quality": 95, "subsampling": 0, "restart_marker_blocks": 2}),
+                          ("grey.jpg", PIL.fromarray(rgb[..., 0], "L"), {"quality": 50})):
         p = os.path.join(d, name)
         img.save(p, **kw)
         paths.append(p)
@@ -101,7 +105,7 @@ def test_image_decoders_and_png_writer(driver, tmp_path):
 def test_scene_loader_and_bvh_builders(driver, tmp_path, name):
     root = make_root(tmp_path)
     scene = root / "res" / "scene" / f"{name}.json"
-    args = [root, scene] + (["res\\texture\\yokohama", "bmp"] if name == "micro_surface" else [])
+    args = [root, scene]
     out = run(driver, "scene", *args)
     assert out.count(": rc") == 0, out  # every builder, leaf sizes 1 and 3
     for p in corrupt_copies(str(scene), str(tmp_path)):
