@@ -6,8 +6,9 @@ A step is one frame: 8 passes (batched into one persistent HIP launch plus an in
 over the 1920x1080 frame and the 8-bit gamma output; with N > 1 each rank renders its interleaved 8-row bands and
 rank 0 gathers the ranks' rows of the float accumulation buffer with one RCCL gather (torch.distributed
 "nccl"; PT_FRAME_COLLECTIVE=reduce: one reduce of the whole buffer instead), after which rank 0
-writes the 8-bit image. Frames are queued with no host synchronisation on three renderer contexts,
-each launching on half the grid, so one frame's tail overlaps the next frames' work (PT_BENCH_INFLIGHT=1:
+writes the 8-bit image. Frames are queued with no host synchronisation on three renderer contexts
+(five when tiled), each launching on half (a quarter of) the grid, so one frame's tail overlaps the
+next frames' work (PT_BENCH_INFLIGHT=1:
 one at a time on the whole grid); the host-synchronised single-frame latency is reported beside it. Mrays/s = ray segments traced (the live-ray counts the
 reference's thread_shrink returns, summed over passes and depths and over ranks) / wall time.
 
@@ -203,6 +204,10 @@ def main() -> int:
         if world == 1 and args.gpus > 1:
             return 2
 
+    # HIP hardware queues per process (read when HIP initialises, before any device call): with the
+    # default 4, more than three frames in flight share queues and serialise (4 frames on 33 % grids:
+    # 7.89 ms at N = 1); with 8 they overlap (profiles/r02/scaling/hw_queues.txt)
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     import torch
     import torch.distributed as dist
 
@@ -220,12 +225,13 @@ def main() -> int:
         else:
             dist.init_process_group(backend)
     # frames in flight: one renderer context (own stream, image and pass buffers) per frame in flight,
-    # so the next frame's workgroups fill the previous frame's tail; 1 = one at a time
-    inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or 3
-    # with three frames in flight each launch takes half the occupancy-sized grid (pt_set_grid_share):
-    # 6.35 vs 6.58 ms/frame at N = 1 (two in flight, whole grid), 1.10 vs 1.36 ms for an 8-way share
-    # (profiles/r02/scaling/grid_share.txt)
-    grid_share = int(os.environ.get("PT_BENCH_GRID_SHARE", "50")) if inflight >= 3 else 100
+    # so the next frame's workgroups fill the previous frame's tail; 1 = one at a time.
+    # Each launch takes 1 / (F - 1) of the occupancy-sized grid (pt_set_grid_share). Measured best
+    # (profiles/r02/scaling/hw_queues.txt, ms per frame of rank 0's share): three frames on half grids
+    # for the whole frame (6.04 vs 6.13 with five), five on quarter grids for a tiled share (0.99 vs 1.08
+    # at N = 8, 1.76 vs 1.80 at N = 4, 3.24 vs 3.26 at N = 2)
+    inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or (3 if world == 1 else 5)
+    grid_share = int(os.environ.get("PT_BENCH_GRID_SHARE", "0")) or (100 // (inflight - 1) if inflight >= 3 else 100)
     wl = Workload(args.workload)
     scene, cfg, cam = wl.scene, wl.cfg, wl.cam
     width, height, spp = wl.width, wl.height, wl.spp

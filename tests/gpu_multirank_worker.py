@@ -1,9 +1,10 @@
 """Worker of tests/test_gpu_multirank.py, launched N times by torch.distributed.run on ONE GPU (every
 rank on cuda:0, gloo between them): the bench.py frame pipeline (TiledFrame over renderer contexts,
-two frames in flight, rank 0 collecting the frame) on the HIP renderer. Rank 0 saves each context's
-float image and 8-bit image for the test to compare with the oracle.
+INFLIGHT frames in flight, each launch on 1 / (INFLIGHT - 1) of the grid from three on and the last
+frame on the whole grid, rank 0 collecting the frame) on the HIP renderer. Rank 0 saves each
+context's float image and 8-bit image for the test to compare with the oracle.
 
-    worker.py OUT_PREFIX COLLECTIVE FRAMES
+    worker.py OUT_PREFIX COLLECTIVE FRAMES [INFLIGHT]
 """
 import os
 import sys
@@ -24,6 +25,8 @@ def scene():
 
 def main() -> int:
     out, collective, frames = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    inflight = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+    share = 100 // (inflight - 1) if inflight >= 3 else 100
     import torch.distributed as dist
 
     import pathtracerwithcuda_amd as pt
@@ -34,13 +37,17 @@ def main() -> int:
     cfg = pt.configuration(max_tracer_depth=8)
     cam = pt.camera(W, H, **CAM)
     rs, fr = [], []
-    for _ in range(2):  # two frames in flight, one renderer context each (bench.py)
+    for _ in range(inflight):  # one renderer context per frame in flight (bench.py)
         r = pt.Renderer(0)
+        r.set_grid_share(share)
         r.upload(sc, cfg)
         rs.append(r)
         fr.append(pt.TiledFrame(r, W, H, dist, 8, device="cuda:0", collective=collective))
     for i in range(frames):
-        fr[i % 2].launch(cam, cfg, SPP)
+        last = i == frames - 1 and share < 100
+        if last:
+            rs[i % inflight].set_grid_share(100)
+        fr[i % inflight].launch(cam, cfg, SPP)
     for f in fr:
         f.synchronize()
     if rank == 0:

@@ -1,6 +1,6 @@
 """The N > 1 frame pipeline on the HIP renderer: 2 and 3 ranks, every rank on cuda:0 (this pool's boxes
 have one GPU), gloo between the ranks, through the same TiledFrame/renderer code bench.py runs with
-RCCL on an 8-GPU node (band tiling, two frames in flight on their own HIP streams, the frame's one
+RCCL on an 8-GPU node (band tiling, two or five frames in flight on their own HIP streams, the frame's one
 collective — a gather of the ranks' rows or a reduce of the float buffer — and rank 0's 8-bit
 output). Rank 0's images must equal the oracle's single-frame render bit for bit."""
 import os
@@ -26,12 +26,12 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("ranks,collective", [(2, "gather"), (3, "reduce")])
-def test_tiled_frames_on_hip_equal_the_oracle(require_gpu, tmp_path, ranks, collective):
+@pytest.mark.parametrize("ranks,collective,inflight", [(2, "gather", 5), (3, "reduce", 2)])
+def test_tiled_frames_on_hip_equal_the_oracle(require_gpu, tmp_path, ranks, collective, inflight):
     out = str(tmp_path / "mr")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(HERE, "gpu_multirank_worker.py"), out, collective, "5"]
+           os.path.join(HERE, "gpu_multirank_worker.py"), out, collective, str(2 * inflight + 1), str(inflight)]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     assert res.returncode == 0, res.stderr[-4000:]
@@ -39,7 +39,7 @@ def test_tiled_frames_on_hip_equal_the_oracle(require_gpu, tmp_path, ranks, coll
     cfg = pt.configuration(max_tracer_depth=8)
     cam = pt.camera(worker.W, worker.H, **worker.CAM)
     ref, ref8, _ = oracle.render(sc.view, cam, cfg, 1, worker.SPP)
-    for k in range(2):
+    for k in range(inflight):
         img = np.load(f"{out}_{k}_f.npy")
         img8 = np.load(f"{out}_{k}_u8.npy")
         assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), f"context {k}: float image"

@@ -557,11 +557,12 @@ def test_edge_cases(gpu, case):
     assert_bitwise(img8.reshape(-1, 3), ref8, f"{case} 8-bit")
 
 
-@pytest.mark.parametrize("inflight", [2, 3])
+@pytest.mark.parametrize("inflight", [2, 3, 5])
 def test_frames_in_flight_equal_one_at_a_time(require_gpu, inflight):
     """bench.py's frame pipeline: frames queued on several contexts with no host sync between them
-    (TiledFrame.launch) each end with the image of a frame rendered on its own, bit for bit; with three
-    contexts each launches on half the grid and the last frame on the whole grid, as bench.py does."""
+    (TiledFrame.launch) each end with the image of a frame rendered on its own, bit for bit; with F >= 3
+    contexts each launches on 1 / (F - 1) of the grid and the last frame on the whole grid, as bench.py
+    does (three for the whole frame, five for a tiled share)."""
     sc = pt.cornell_scene(pt.torus_knot(80, 24), cube_length=32)
     cfg = pt.configuration(max_tracer_depth=8)
     cam = pt.camera(96, 64, **BENCH_CAM)
@@ -572,7 +573,7 @@ def test_frames_in_flight_equal_one_at_a_time(require_gpu, inflight):
         for q in rs:
             q.upload(sc, cfg)
             if inflight >= 3:
-                q.set_grid_share(50)
+                q.set_grid_share(100 // (inflight - 1))
             frames.append(pt.TiledFrame(q, 96, 64))
         n = 2 * inflight + 1
         for i in range(n):
