@@ -4,15 +4,15 @@
 // FreeImage 3.17 decodes with its bundled IJG libjpeg 9a. Without JPEG_ACCURATE in the flags (the
 // reference passes 0), its loader asks libjpeg for the fast integer IDCT and no fancy upsampling.
 // That output is restated here:
-//   - baseline and extended-sequential Huffman scans (SOF0/SOF1, 8-bit), interleaved or not, restart
-//     intervals, 1 (grey) or 3 (YCbCr, or RGB by Adobe transform 0 / component ids 'R','G','B')
-//     components;
+//   - baseline, extended-sequential and progressive Huffman scans (SOF0/SOF1/SOF2, 8-bit; spectral
+//     selection, successive approximation, end-of-band runs), interleaved or not, restart intervals,
+//     1 (grey) or 3 (YCbCr, or RGB by Adobe transform 0 / component ids 'R','G','B') components;
 //   - the AAN "ifast" IDCT (jidctfst.c) on the scaled quantisation table of jddctmgr.c;
 //   - chroma replicated to full size (jdsample.c int_upsample; jdmerge.c merged upsampling is the
 //     same arithmetic);
 //   - the integer YCbCr -> RGB tables of jdcolor.c.
 // Grey images come out as r = g = b (FreeImage_ConvertTo24Bits of an 8-bit grey bitmap).
-// Progressive, arithmetic-coded, lossless, 12-bit and CMYK files are rejected with an error.
+// Arithmetic-coded, lossless, hierarchical, 12-bit and CMYK files are rejected with an error.
 //
 // Two arithmetic variants (pt_jpeg_decode):
 //   PT_JPEG_IJG9 — libjpeg 9a, what the reference ran (the default of pt_image_load). Its IDCT
@@ -259,8 +259,115 @@ void idct_ifast(const int16_t* in, const int* q, uint8_t* out, int stride) {
 
 inline uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
 
+// One scan's parameters: progressive frames code the coefficients in bands (Ss..Se) and bit planes
+// (Ah: the previous scan's low bit, Al: this scan's), jdphuff.c; sequential scans take every
+// coefficient of a block at once (jdhuff.c decode_mcu).
+struct ScanSpec {
+    bool prog;
+    int ss, se, ah, al;
+};
+
+void block_sequential(Bits& br, Comp& cp, int16_t* blk, const Huff* dc_t, const Huff* ac_t) {
+    int s = br.decode(dc_t[cp.td]);
+    if (s > 15) s = 15;  // corrupt table value (a baseline DC size is at most 11)
+    int diff = 0;
+    if (s) diff = extend(br.bits(s), s);
+    cp.dc_pred = (int)((unsigned)cp.dc_pred + (unsigned)diff);  // libjpeg's int, wrapped
+    blk[0] = (int16_t)cp.dc_pred;
+    for (int k = 1; k < 64; k++) {
+        const int rs = br.decode(ac_t[cp.ta]);
+        const int r = rs >> 4, sz = rs & 15;
+        if (sz) {
+            k += r;
+            blk[kNatural[k]] = (int16_t)extend(br.bits(sz), sz);
+        } else {
+            if (r != 15) break;
+            k += 15;
+        }
+    }
+}
+
+// jdphuff.c decode_mcu_DC_first / _DC_refine
+void block_dc_prog(Bits& br, Comp& cp, int16_t* blk, const Huff* dc_t, const ScanSpec& sp) {
+    if (sp.ah == 0) {
+        int s = br.decode(dc_t[cp.td]);
+        if (s > 15) s = 15;
+        int diff = 0;
+        if (s) diff = extend(br.bits(s), s);
+        cp.dc_pred = (int)((unsigned)cp.dc_pred + (unsigned)diff);
+        blk[0] = (int16_t)((unsigned)cp.dc_pred << sp.al);
+    } else if (br.bits(1)) {
+        blk[0] = (int16_t)(blk[0] | (1 << sp.al));
+    }
+}
+
+// jdphuff.c decode_mcu_AC_first: one band of one block, or one block of an end-of-band run
+void block_ac_first(Bits& br, const Comp& cp, int16_t* blk, const Huff* ac_t, const ScanSpec& sp, unsigned& eobrun) {
+    if (eobrun > 0) {
+        eobrun--;
+        return;
+    }
+    for (int k = sp.ss; k <= sp.se; k++) {
+        const int rs = br.decode(ac_t[cp.ta]);
+        int r = rs >> 4;
+        const int sz = rs & 15;
+        if (sz) {
+            k += r;
+            blk[kNatural[k]] = (int16_t)((unsigned)extend(br.bits(sz), sz) << sp.al);
+        } else if (r == 15) {
+            k += 15;
+        } else {
+            eobrun = 1u << r;
+            if (r) eobrun += (unsigned)br.bits(r);
+            eobrun--;
+            break;
+        }
+    }
+}
+
+// jdphuff.c decode_mcu_AC_refine: correction bits for the coefficients already nonzero, and the
+// newly nonzero ones (magnitude 1 << Al) placed after their run of still-zero coefficients
+void block_ac_refine(Bits& br, const Comp& cp, int16_t* blk, const Huff* ac_t, const ScanSpec& sp, unsigned& eobrun) {
+    const int p1 = 1 << sp.al, m1 = -(1 << sp.al);
+    auto correct = [&](int16_t& c) {
+        if (br.bits(1) && (c & p1) == 0) c = (int16_t)(c >= 0 ? c + p1 : c + m1);
+    };
+    int k = sp.ss;
+    if (eobrun == 0) {
+        for (; k <= sp.se; k++) {
+            const int rs = br.decode(ac_t[cp.ta]);
+            int r = rs >> 4;
+            int s = rs & 15;
+            if (s) {
+                s = br.bits(1) ? p1 : m1;  // the new coefficient's sign (its size is 1)
+            } else if (r != 15) {
+                eobrun = 1u << r;
+                if (r) eobrun += (unsigned)br.bits(r);
+                break;  // the rest of the band is handled by the end-of-band logic below
+            }
+            do {
+                int16_t& c = blk[kNatural[k]];
+                if (c != 0) {
+                    correct(c);
+                } else if (--r < 0) {
+                    break;  // the zero coefficient that becomes nonzero
+                }
+                k++;
+            } while (k <= sp.se);
+            if (s) blk[kNatural[k]] = (int16_t)s;
+        }
+    }
+    if (eobrun > 0) {
+        for (; k <= sp.se; k++) {
+            int16_t& c = blk[kNatural[k]];
+            if (c != 0) correct(c);
+        }
+        eobrun--;
+    }
+}
+
 bool decode_scan(Bits& br, std::vector<Comp>& comps, const std::vector<int>& sc, const Huff* dc_t, const Huff* ac_t,
-                 int mcux, int mcuy, int restart_interval) {
+                 int mcux, int mcuy, int restart_interval, const ScanSpec& sp) {
     const bool inter = sc.size() > 1;
     int nx, ny;
     if (inter) {
@@ -271,6 +378,7 @@ bool decode_scan(Bits& br, std::vector<Comp>& comps, const std::vector<int>& sc,
         ny = comps[sc[0]].hib;
     }
     for (int c : sc) comps[c].dc_pred = 0;
+    unsigned eobrun = 0;
     const long total = (long)nx * ny;
     int todo = restart_interval;
     for (long m = 0; m < total; m++) {
@@ -278,6 +386,7 @@ bool decode_scan(Bits& br, std::vector<Comp>& comps, const std::vector<int>& sc,
             if (todo == 0) {
                 br.restart();
                 for (int c : sc) comps[c].dc_pred = 0;
+                eobrun = 0;
                 todo = restart_interval;
             }
             todo--;
@@ -290,24 +399,10 @@ bool decode_scan(Bits& br, std::vector<Comp>& comps, const std::vector<int>& sc,
                 for (int bx = 0; bx < bwid; bx++) {
                     const int col = mx * bwid + bx, row = my * bh + by;
                     int16_t* blk = &cp.coef[((size_t)row * cp.bw + col) * 64];
-                    // jdhuff.c decode_mcu (baseline): DC difference, then run/size AC pairs
-                    int s = br.decode(dc_t[cp.td]);
-                    if (s > 15) s = 15;  // corrupt table value (a baseline DC size is at most 11)
-                    int diff = 0;
-                    if (s) diff = extend(br.bits(s), s);
-                    cp.dc_pred = (int)((unsigned)cp.dc_pred + (unsigned)diff);  // libjpeg's int, wrapped
-                    blk[0] = (int16_t)cp.dc_pred;
-                    for (int k = 1; k < 64; k++) {
-                        const int rs = br.decode(ac_t[cp.ta]);
-                        const int r = rs >> 4, sz = rs & 15;
-                        if (sz) {
-                            k += r;
-                            blk[kNatural[k]] = (int16_t)extend(br.bits(sz), sz);
-                        } else {
-                            if (r != 15) break;
-                            k += 15;
-                        }
-                    }
+                    if (!sp.prog) block_sequential(br, cp, blk, dc_t, ac_t);
+                    else if (sp.ss == 0) block_dc_prog(br, cp, blk, dc_t, sp);
+                    else if (sp.ah == 0) block_ac_first(br, cp, blk, ac_t, sp, eobrun);
+                    else block_ac_refine(br, cp, blk, ac_t, sp, eobrun);
                 }
         }
     }
@@ -326,7 +421,7 @@ bool decode_jpeg(const unsigned char* d, size_t n, int variant, int* out_w, int*
     Huff dc_t[4], ac_t[4];
     std::vector<Comp> comps;
     int W = 0, H = 0, hmax = 1, vmax = 1, mcux = 0, mcuy = 0, restart_interval = 0;
-    bool frame = false, jfif = false, adobe = false, any_scan = false;
+    bool frame = false, prog = false, jfif = false, adobe = false, any_scan = false;
     int adobe_transform = -1;
     size_t p = 2;
     while (p + 4 <= n) {
@@ -341,7 +436,8 @@ bool decode_jpeg(const unsigned char* d, size_t n, int variant, int* out_w, int*
         if (len < 2 || p + len > n) { err = "truncated JPEG segment"; return false; }
         const uint8_t* s = d + p + 2;
         const size_t sl = len - 2;
-        if (m == 0xC0 || m == 0xC1) {
+        if (m == 0xC0 || m == 0xC1 || m == 0xC2) {
+            prog = m == 0xC2;
             if (sl < 6 || s[0] != 8) { err = "only 8-bit JPEG is supported"; return false; }
             H = be16(s + 1);
             W = be16(s + 3);
@@ -376,9 +472,8 @@ bool decode_jpeg(const unsigned char* d, size_t n, int variant, int* out_w, int*
                 c.coef.assign((size_t)c.bw * c.bh * 64, 0);
             }
             frame = true;
-        } else if ((m >= 0xC2 && m <= 0xC3) || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
-                   (m >= 0xCD && m <= 0xCF)) {
-            err = m == 0xC2 ? "progressive JPEG is not supported" : "this JPEG coding process is not supported";
+        } else if (m == 0xC3 || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) || (m >= 0xCD && m <= 0xCF)) {
+            err = "this JPEG coding process (lossless, hierarchical or arithmetic) is not supported";
             return false;
         } else if (m == 0xC4) {
             size_t q = 0;
@@ -412,6 +507,13 @@ bool decode_jpeg(const unsigned char* d, size_t n, int variant, int* out_w, int*
             if (!frame) { err = "JPEG scan before frame"; return false; }
             const int ns = sl ? s[0] : 0;
             if (ns < 1 || ns > 4 || sl < 1 + 2 * (size_t)ns + 3) { err = "bad JPEG scan header"; return false; }
+            ScanSpec sp{prog, s[1 + 2 * ns], s[2 + 2 * ns], s[3 + 2 * ns] >> 4, s[3 + 2 * ns] & 15};
+            if (prog && (sp.se > 63 || sp.ss > sp.se || (sp.ss == 0 && sp.se != 0) || (sp.ss > 0 && ns != 1) ||
+                         sp.al > 13 || (sp.ah != 0 && sp.ah != sp.al + 1))) {
+                err = "bad progressive JPEG scan";
+                return false;
+            }
+            const bool need_dc = !prog || (sp.ss == 0 && sp.ah == 0), need_ac = !prog || sp.ss > 0;
             std::vector<int> sc;
             for (int i = 0; i < ns; i++) {
                 const int cid = s[1 + 2 * i];
@@ -421,14 +523,15 @@ bool decode_jpeg(const unsigned char* d, size_t n, int variant, int* out_w, int*
                 if (ci < 0) { err = "bad JPEG scan component"; return false; }
                 comps[ci].td = s[2 + 2 * i] >> 4;
                 comps[ci].ta = s[2 + 2 * i] & 15;
-                if (comps[ci].td > 3 || comps[ci].ta > 3 || !dc_t[comps[ci].td].defined || !ac_t[comps[ci].ta].defined) {
+                if (comps[ci].td > 3 || comps[ci].ta > 3 || (need_dc && !dc_t[comps[ci].td].defined) ||
+                    (need_ac && !ac_t[comps[ci].ta].defined)) {
                     err = "JPEG Huffman table missing";
                     return false;
                 }
                 sc.push_back(ci);
             }
             Bits br{d, n, p + len};
-            decode_scan(br, comps, sc, dc_t, ac_t, mcux, mcuy, restart_interval);
+            decode_scan(br, comps, sc, dc_t, ac_t, mcux, mcuy, restart_interval, sp);
             any_scan = true;
             // continue after the entropy-coded data: the next marker that is not RSTn
             size_t q = br.pos;

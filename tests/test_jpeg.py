@@ -53,6 +53,15 @@ def cases():
     out.append(("grey", encode(PIL.fromarray(noisy[..., 1], "L"), quality=70)))
     out.append(("tiny", encode(PIL.fromarray(noisy[:5, :3], "RGB"), quality=90)))
     out.append(("q100_444", encode(rgb, quality=100, subsampling=0)))
+    # progressive (SOF2): spectral selection and successive approximation scans, end-of-band runs
+    for sub in (0, 2):
+        out.append((f"prog_sub{sub}", encode(rgb, quality=80, subsampling=sub, progressive=True)))
+    out.append(("prog_optimized", encode(rgb, quality=40, progressive=True, optimize=True)))
+    out.append(("prog_restart", encode(rgb, quality=90, progressive=True, restart_marker_blocks=5)))
+    out.append(("prog_grey", encode(PIL.fromarray(noisy[..., 2], "L"), quality=85, progressive=True)))
+    flat = np.zeros((40, 48, 3), np.uint8)
+    flat[8:30, 10:40] = (200, 40, 90)  # long end-of-band runs
+    out.append(("prog_flat", encode(PIL.fromarray(flat, "RGB"), quality=75, progressive=True)))
     return out
 
 
@@ -84,8 +93,11 @@ def test_load_image_decodes_jpeg_as_libjpeg_9a(tmp_path):
 
 def test_unsupported_jpegs_fail_loudly(tmp_path):
     rgb = PIL.fromarray(np.zeros((16, 16, 3), np.uint8), "RGB")
-    p = tmp_path / "prog.jpg"
-    rgb.save(str(p), progressive=True)
+    data = bytearray(encode(rgb))
+    i = data.index(b"\xff\xc0")
+    data[i + 1] = 0xC9  # the same frame marked arithmetic-coded
+    p = tmp_path / "arith.jpg"
+    p.write_bytes(bytes(data))
     with pytest.raises(pt.PtError):
         pt.load_image(str(p))
     p = tmp_path / "cmyk.jpg"

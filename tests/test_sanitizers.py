@@ -83,7 +83,10 @@ def _images(d):
                           ("rgb420.jpg", PIL.fromarray(rgb, "RGB"), {"quality": 80, "subsampling": 2}),
                           ("rgb444_rst.jpg", PIL.fromarray(rgb, "RGB"),
                            {"quality": 95, "subsampling": 0, "restart_marker_blocks": 2}),
-                          ("grey.jpg", PIL.fromarray(rgb[..., 0], "L"), {"quality": 50})):
+                          ("grey.jpg", PIL.fromarray(rgb[..., 0], "L"), {"quality": 50}),
+                          ("prog.jpg", PIL.fromarray(rgb, "RGB"), {"quality": 70, "progressive": True}),
+                          ("prog_rst.jpg", PIL.fromarray(rgb, "RGB"),
+                           {"quality": 90, "progressive": True, "restart_marker_blocks": 3})):
         p = os.path.join(d, name)
         img.save(p, **kw)
         paths.append(p)
