@@ -3,6 +3,7 @@ hand-written JSON, OBJ, BMP/TGA/PNG (zlib-fed) parsers and the BVH builders (pt_
 pt_host.cpp), linked into tools/san/san_driver with -fsanitize=address,undefined, run over the
 reference's own fixtures (tests/golden/res) and over truncated and bit-flipped copies of every file.
 Loaders may reject corrupted input (that is their error path); a sanitizer report or a crash fails."""
+import fcntl
 import os
 import subprocess
 
@@ -19,7 +20,11 @@ PIL = pytest.importorskip("PIL.Image")
 
 @pytest.fixture(scope="module")
 def driver():
-    subprocess.run(["make", "-s", "-C", SAN], check=True, capture_output=True)
+    # one build at a time when pytest-xdist workers share the tree (make relinks a running driver otherwise)
+    os.makedirs(os.path.join(SAN, "build"), exist_ok=True)
+    with open(os.path.join(SAN, "build", ".lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", SAN], check=True, capture_output=True)
     return DRIVER
 
 
