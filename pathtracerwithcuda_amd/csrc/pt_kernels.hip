@@ -43,6 +43,11 @@ namespace pt {
 #ifndef PT_ROOT_SKIP
 #define PT_ROOT_SKIP 1
 #endif
+// PT_DEFER: pass_kernel_u lanes walk on past a passing leaf and test its triangle later (pt_path.h,
+// "deferred leaves"), so triangle batches wait for more lanes without parking them
+#ifndef PT_DEFER
+#define PT_DEFER 0
+#endif
 template <class T>
 __device__ __forceinline__ void opaque(T& x) {
     int* p = reinterpret_cast<int*>(&x);
@@ -441,6 +446,12 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     MeshWalk w;
     int mesh = 0;
     int ptri = -1;  // leaf triangle awaiting its test (LANE_TRI)
+    // DEF: deferred leaves (binary walk with prefetched triangles). dtri: the deferred leaf's triangle, -1
+    // none, -2 the lane cannot defer (non-finite 1/d, or boxes not nested); de its box entry; pe the entry
+    // of the leaf a lane is parked on (LANE_TRI; ptri -1: parked at its mesh's end behind a deferred leaf)
+    constexpr bool DEF = PT_DEFER && CHAIN == 2 && PF && !QN && !WIDE;
+    int dtri = -2;
+    float de = 0.0f, pe = 0.0f;
     unsigned int unit = 0;
     int32_t pseed = 0;
     int depth = 0;
@@ -568,6 +579,9 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         if (mode == LANE_NEW) {
             if (roots) mode = begin_segment_roots(sc, lds_mesh, lds_root, ps, inv, h, w, mesh);
             else mode = begin_segment<WIDE>(sc, lds_mesh, ps, inv, h, w, mesh);
+            if (DEF)
+                dtri = sc.nested && __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z)
+                           ? -1 : -2;
         }
         if (!__any(mode != LANE_DONE)) break;
         if (PROF) { const unsigned long long t = __builtin_readcyclecounter(); prof[8] += t - tc; tc = t; }
@@ -659,12 +673,28 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     opaque(w2); opaque(l2); opaque(t2);
                 }
                 bool leaf;
+                float le = 0.0f;
                 if (WIDE && w.end < 0) leaf = walk_wide(rw, ps.o, inv, w, ptri);
                 else leaf = QN ? walk_box_q(rq, fb, fs, ps.o, inv, w, ptri)
-                               : (CHAIN > 1 ? walk_box_chain<CHAIN>(rn, ps.o, inv, w, ptri) : walk_box(rn, ps.o, inv, w, ptri));
-                if (leaf) {
+                               : (CHAIN > 1 ? walk_box_chain<CHAIN>(rn, ps.o, inv, w, ptri, le) : walk_box(rn, ps.o, inv, w, ptri));
+                if (DEF) {
+                    // a lane without a deferred leaf defers this one: it walks on past it, the triangle's loads
+                    // in flight until its batch; with one deferred already (or unable to defer) it parks.
+                    // Selects rather than branches: the exec-mask bookkeeping of a branchy form costs more
+                    // scalar issue than the batching saves
+                    const bool defer = leaf && dtri == -1;
+                    if (leaf && dtri < 0) {
+                        pta = bload(rt, ptri * 48); ptb = bload(rt, ptri * 48 + 16); ptc = bload(rt, ptri * 48 + 32);
+                    }
+                    dtri = defer ? ptri : dtri;
+                    de = defer ? le : de;
+                    pe = le;
+                    w.pos += defer ? 1 : 0;
+                    mode = leaf && !defer ? LANE_TRI : mode;
+                } else if (leaf) {
                     mode = LANE_TRI;
-                    if (PF && !QN) {  // the triangle's loads are in flight while the batch fills
+                    pe = le;
+                    if (PF && !QN && (!DEF || dtri < 0)) {  // the triangle's loads are in flight while the batch fills
                         pta = bload(rt, ptri * 48); ptb = bload(rt, ptri * 48 + 16); ptc = bload(rt, ptri * 48 + 32);
                     }
                 } else if (!PT_MESH_SITE && w.pos == w.end) {
@@ -673,12 +703,37 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             }
             // leaf triangles are tested in batches of at least tri_min lanes (or when no lane can
             // walk on): the triangle test then runs with many lanes active instead of one or two
-            const unsigned long long pend = __ballot(mode == LANE_TRI);
+            const bool in_batch = mode == LANE_TRI || (DEF && dtri >= 0);
+            const unsigned long long pend = __ballot(in_batch);
             // PF: no lane leaves the walk loop parked, so the prefetched geometry never lives across shading
             if (pend && (__popcll(pend) >= (unsigned int)tri_min || !__any(mode == LANE_WALK) ||
                          (PF && k == walk_steps - 1))) {
                 if (PROF) { prof[5]++; prof[6] += (unsigned long long)__popcll(pend); }
-                if (mode == LANE_TRI) {
+                if (DEF) {
+                    if (in_batch) {
+                        // the earliest unresolved leaf: the deferred one, else the one the lane is parked on;
+                        // it counts if its box still passes under the min_t its preorder position sees
+                        const bool d = dtri >= 0;
+                        walk_tri_geom_if(pta, ptb, ptc, ps.o, ps.d, w, d ? dtri : ptri, (d ? de : pe) <= w.t);
+                        // a second leaf parked behind the deferred one becomes the deferred leaf if its box
+                        // still passes (a leaf's skip index is the next record: pos + 1 either way); a lane
+                        // parked at its mesh's end (ptri -1) stays there for mesh_done
+                        const bool parked = mode == LANE_TRI;
+                        const int nt = parked && d && ptri >= 0 && pe <= w.t ? ptri : -1;
+                        w.pos += parked && (!d || ptri >= 0) ? 1 : 0;
+                        mode = parked ? LANE_WALK : mode;
+                        dtri = d ? nt : dtri;
+                        de = pe;
+                        if (nt >= 0) {
+                            pta = bload(rt, nt * 48); ptb = bload(rt, nt * 48 + 16); ptc = bload(rt, nt * 48 + 32);
+                        }
+                    }
+                    // the round's last step: no lane leaves the walk loop with a deferred leaf
+                    if (k == walk_steps - 1 && dtri >= 0) {
+                        walk_tri_geom_if(pta, ptb, ptc, ps.o, ps.d, w, dtri, de <= w.t);
+                        dtri = -1;
+                    }
+                } else if (mode == LANE_TRI) {
                     if (QN) walk_tri_q(rn, rt, ps.o, ps.d, inv, w, ptri);
                     else {
                         if (PT_DUP == 3) {
@@ -696,8 +751,17 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 }
             }
             // a lane whose mesh walk ended in this step (after a box or after its triangle) merges it and
-            // starts the next mesh: one mesh_done site for both (PT_MESH_SITE=0 builds: two)
-            if (PT_MESH_SITE && mode == LANE_WALK && w.pos == w.end) mesh_done();
+            // starts the next mesh: one mesh_done site for both (PT_MESH_SITE=0 builds: two); with a leaf
+            // still deferred it parks until that leaf is resolved
+            if (DEF) {
+                const bool at_end = mode == LANE_WALK && w.pos == w.end;
+                const bool wait = at_end && dtri >= 0;
+                mode = wait ? LANE_TRI : mode;
+                ptri = wait ? -1 : ptri;
+                if (at_end && !wait) mesh_done();
+            } else if (PT_MESH_SITE && mode == LANE_WALK && w.pos == w.end) {
+                mesh_done();
+            }
         }
         if (PROF) prof[10] += __builtin_readcyclecounter() - tc;
     }
@@ -1425,7 +1489,8 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
         static const int shade_min = env_int("PT_SHADE_MIN", 28, 1, 64);
         static const int walk_steps = env_int("PT_WALK_STEPS", 8, 1, 64);
         const LaunchParams* a0 = params_dev;
-        static const int tri_min = env_int("PT_TRI_MIN", 6, 1, 64);  // measured best with frames in flight
+        // measured best with frames in flight; lanes with a deferred leaf walk on, so their batches wait longer
+        static const int tri_min = env_int("PT_TRI_MIN", PT_DEFER ? 16 : 6, 1, 64);
         static const int walk_min = env_int("PT_WALK_MIN", 8, 0, 64);
         // PT_TAIL_SHADE_MIN / PT_TAIL_WALK_MIN: the shading thresholds of a wave once the work is drained
         static const int tail_shade = env_int("PT_TAIL_SHADE_MIN", shade_min, 1, 64);

@@ -486,8 +486,9 @@ __device__ __forceinline__ void chain_load(const __amdgpu_buffer_rsrc_t rn, int 
 #pragma unroll
     for (int i = 1; i < CHAIN; i++) asm volatile("" ::"v"(r.lo[i].w), "v"(r.hi[i].w));
 }
+// le: the entry of the leaf box that parks the lane (pass_kernel_u's deferred triangle tests)
 template <int CHAIN>
-__device__ __forceinline__ bool chain_test(const ChainRecs<CHAIN>& r, v3 o, v3 inv, MeshWalk& w, int& tri) {
+__device__ __forceinline__ bool chain_test(const ChainRecs<CHAIN>& r, v3 o, v3 inv, MeshWalk& w, int& tri, float& le) {
 #pragma unroll
     for (int i = 0; i < CHAIN; i++) {
         float entry;
@@ -495,6 +496,7 @@ __device__ __forceinline__ bool chain_test(const ChainRecs<CHAIN>& r, v3 o, v3 i
             const int slot = f2i(r.hi[i].w);
             if (slot >= 0) {
                 tri = slot;
+                le = entry;
                 return true;
             }
             w.pos++;
@@ -526,11 +528,17 @@ __device__ __forceinline__ bool chain_test_flat2(const ChainRecs<2>& r, v3 o, v3
 }
 
 template <int CHAIN>
-__device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri) {
+__device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri,
+                                               float& le) {
     ChainRecs<CHAIN> r;
     chain_load<CHAIN>(rn, w.pos, r);
     if constexpr (CHAIN == 2 && PT_CHAIN_FLAT) return chain_test_flat2(r, o, inv, w, tri);
-    return chain_test<CHAIN>(r, o, inv, w, tri);
+    return chain_test<CHAIN>(r, o, inv, w, tri, le);
+}
+template <int CHAIN>
+__device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri) {
+    float le;
+    return walk_box_chain<CHAIN>(rn, o, inv, w, tri, le);
 }
 
 // ---- the wide walk (pt_scene.h `wide`, built by pt_runtime.cpp build_wide) ------------------------
@@ -596,6 +604,19 @@ __device__ __forceinline__ bool walk_wide(const __amdgpu_buffer_rsrc_t rw, v3 o,
     return true;
 }
 
+// ---- deferred leaves (pass_kernel_u, PT_DEFER) ----------------------------------------------------
+// A lane whose walk reaches a passing leaf need not wait for that leaf's triangle test: it can record
+// the leaf (its triangle and its box entry) and walk on under the min_t it has, which is then at least
+// the reference's. Exactness, for a lane whose 1/d is finite in a scene whose boxes are nested (every
+// node's box contains its children's, DevScene::nested): the slab arithmetic is monotone in the box
+// planes, so a box that passes under some min_t has every ancestor pass under any larger one (the wide
+// walk's argument). Walking under a larger min_t therefore visits every node the reference visits, in
+// the same preorder, plus nodes it would skip; the leaves it reaches are tested later, in preorder, and
+// each counts only if its own test passes under the min_t the reference would have at that leaf
+// (`entry <= min_t`, re-checked when its triangle is tested) — exactly the leaves the reference tests,
+// with the same results. A lane holds one deferred leaf; reaching a second one it parks until the
+// first is resolved, and a mesh walk that ends with a deferred leaf merges only after it is resolved.
+//
 // walk_tri with the triangle's records already loaded. `advance`: the binary walk moves to pos + 1
 // after the leaf; the wide walk already holds the position after it (walk_wide).
 __device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri,
@@ -605,6 +626,17 @@ __device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o
         w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
     }
     if (advance) w.pos++;
+}
+
+// walk_tri_geom without advancing, the hit accepted only where `counts` (a deferred leaf whose box still
+// passes under the current min_t, pass_kernel_u's DEF walk): the test runs for every lane of the batch
+__device__ __forceinline__ void walk_tri_geom_if(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri,
+                                                 bool counts) {
+    float t, t1, t2;
+    const bool hit = triangle_test(a, b, c, o, d, &t, &t1, &t2);
+    if (counts && hit && t > 0.0f && t < w.t) {
+        w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
+    }
 }
 
 __device__ __forceinline__ void walk_tri(const __amdgpu_buffer_rsrc_t rt, v3 o, v3 d, MeshWalk& w, int tri,

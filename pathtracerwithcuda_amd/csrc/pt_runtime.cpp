@@ -581,6 +581,38 @@ void free_scene(pt_context* ctx) {
     std::memset(&ctx->scene, 0, sizeof(ctx->scene));
 }
 
+// Whether every internal node's box contains both children's boxes, per axis as intervals, in every mesh
+// (preorder records: the left child is n + 1, the right child the left child's skip index when it lies
+// before n's own). pass_kernel_u's deferred triangle tests rest on it (pt_path.h, "deferred leaves"). The
+// reference's builders merge child boxes with min/max, so it holds for their trees; a refit by position
+// and scale (mesh_refit_kernel) maps every corner by the same per-axis monotone function and keeps it.
+int nodes_nested(const std::vector<float4>& nodes, const std::vector<int2>& ranges) {
+    auto lo = [&](int n) { return nodes[2 * (size_t)n]; };
+    auto hi = [&](int n) { return nodes[2 * (size_t)n + 1]; };
+    auto inside = [&](int c, int p) {
+        const float4 cl = lo(c), ch = hi(c), pl = lo(p), ph = hi(p);
+        const float c0[3] = {std::fmin(cl.x, ch.x), std::fmin(cl.y, ch.y), std::fmin(cl.z, ch.z)};
+        const float c1[3] = {std::fmax(cl.x, ch.x), std::fmax(cl.y, ch.y), std::fmax(cl.z, ch.z)};
+        const float p0[3] = {std::fmin(pl.x, ph.x), std::fmin(pl.y, ph.y), std::fmin(pl.z, ph.z)};
+        const float p1[3] = {std::fmax(pl.x, ph.x), std::fmax(pl.y, ph.y), std::fmax(pl.z, ph.z)};
+        for (int a = 0; a < 3; a++)
+            if (!(p0[a] <= c0[a] && c1[a] <= p1[a]) || !std::isfinite(p0[a]) || !std::isfinite(p1[a])) return false;
+        return true;
+    };
+    for (const int2 r : ranges) {
+        for (int n = r.x; n < r.y; n++) {
+            if (__builtin_bit_cast(int, hi(n).w) >= 0) continue;  // leaf
+            const int end = __builtin_bit_cast(int, lo(n).w);
+            const int left = n + 1;
+            if (left >= end || left >= r.y) return 0;
+            if (!inside(left, n)) return 0;
+            const int right = __builtin_bit_cast(int, lo(left).w);
+            if (right < end && right < r.y && !inside(right, n)) return 0;
+        }
+    }
+    return 1;
+}
+
 int upload_stage(pt_context* ctx, const SceneStage& st) {
     struct Piece { const void* src; size_t bytes; size_t off; };
     std::vector<Piece> pieces;
@@ -646,6 +678,7 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
             s.first_wide = st.wide.empty() ? -1 : st.mesh_wide[m];
             break;
         }
+    s.nested = nodes_nested(st.nodes, st.mesh_range);
     ctx->node_num = (int)(st.nodes.size() / 2);
     ctx->wide_num = (int)(st.wide.size() / 8);
     ctx->mesh_range = st.mesh_range;

@@ -87,6 +87,7 @@ struct DevScene {
     int material_num;  // records in `materials`
     int first_mesh;    // first mesh with a non-empty node range (mesh_num if none) and that range:
     int2 first_range;  //   where every trace step's mesh walk starts
+    int nested;        // 1: every node's box contains its children's boxes (pass_kernel_u deferred triangles)
 };
 
 // The subset of Core/configuration.h:9-34 that the kernel reads.
