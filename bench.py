@@ -204,10 +204,12 @@ def main() -> int:
         if world == 1 and args.gpus > 1:
             return 2
 
-    # HIP hardware queues per process (read when HIP initialises, before any device call): with the
-    # default 4, more than three frames in flight share queues and serialise (4 frames on 33 % grids:
-    # 7.89 ms at N = 1); with 8 they overlap (profiles/r02/scaling/hw_queues.txt)
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    # HIP hardware queues per process (read when HIP initialises, before any device call): with 4, more
+    # than three frames in flight share queues and serialise (4 frames on 33 % grids: 7.89 ms at N = 1);
+    # with 8 they overlap (profiles/r02/scaling/hw_queues.txt). The GPU boxes EXPORT GPU_MAX_HW_QUEUES=4,
+    # so the value is set here, not defaulted (PT_BENCH_HW_QUEUES overrides it; at most 32 on this pool)
+    hw_queues = os.environ.get("PT_BENCH_HW_QUEUES", "8")
+    os.environ["GPU_MAX_HW_QUEUES"] = hw_queues
     import torch
     import torch.distributed as dist
 
@@ -381,6 +383,7 @@ def main() -> int:
             "band_rows": BAND_ROWS if world > 1 else None,
             "ms_per_frame": round(ms_per_step, 3),
             "frames_in_flight": inflight,
+            "hw_queues": int(hw_queues),
             "grid_share_pct": grid_share,
             "ms_per_frame_latency": round(latency * 1000.0, 3),
             "camera_samples_per_s_M": round(width * height * spp * args.steps / elapsed / 1e6, 3),
