@@ -207,8 +207,10 @@ def main() -> int:
     # HIP hardware queues per process (read when HIP initialises, before any device call): with 4, more
     # than three frames in flight share queues and serialise (4 frames on 33 % grids: 7.89 ms at N = 1);
     # with 8 they overlap (profiles/r02/scaling/hw_queues.txt). The GPU boxes EXPORT GPU_MAX_HW_QUEUES=4,
-    # so the value is set here, not defaulted (PT_BENCH_HW_QUEUES overrides it; at most 32 on this pool)
-    hw_queues = os.environ.get("PT_BENCH_HW_QUEUES", "8")
+    # so the value is set here, not defaulted (PT_BENCH_HW_QUEUES overrides it; at most 32 on this pool).
+    # Tiled (N > 1): 16, so RCCL's own streams get queues of their own beside the five renderer streams
+    # instead of queueing behind a persistent pass launch (16 and 8 measured equal for the share itself)
+    hw_queues = os.environ.get("PT_BENCH_HW_QUEUES", "16" if world > 1 else "8")
     os.environ["GPU_MAX_HW_QUEUES"] = hw_queues
     import torch
     import torch.distributed as dist
