@@ -261,7 +261,8 @@ def main() -> int:
 
     nframe = 0
 
-    last_full = os.environ.get("PT_BENCH_LAST_FULL", "1") != "0"
+    # PT_BENCH_LAST_FULL: how many frames at the end of a batch take the whole grid (default 1)
+    last_full = int(os.environ.get("PT_BENCH_LAST_FULL", "1"))
 
     def run(k: int) -> None:
         # the last frame of a batch has no frame behind it to fill the CUs its launch leaves: it takes
@@ -269,7 +270,7 @@ def main() -> int:
         nonlocal nframe
         for i in range(k):
             q = frames[nframe % inflight]
-            full = last_full and grid_share < 100 and i == k - 1
+            full = grid_share < 100 and i >= k - last_full
             if full:
                 rs[nframe % inflight].set_grid_share(100)
             q.launch(cam, cfg, spp)
