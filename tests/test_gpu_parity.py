@@ -307,6 +307,18 @@ def test_metric_frame_at_the_bench_launch_shape(bench_gpu):
     assert launches == {0: 1, 3: 1}, launches
 
 
+def test_c3_microfacet_sky_dof_frame(bench_gpu):
+    """BASELINE config C3: six GGX spheres (roughness 0.01..1, a conductor), the skybox and a thin-lens
+    camera at 1920x1080, depth 8. 16 passes run as two batched launches of 8: the second batch's
+    accumulate adds into the running sum the first left (path_tracer_kernel.cu:644-651, pass_counter > 1).
+    Pixel subset against the oracle."""
+    import bench
+    wl = bench.Workload("c3")
+    assert wl.cam.aperture_radius > 0.0 and wl.scene.view.sphere_num == 6
+    launches, _ = _render_workload_subset(bench_gpu, wl, passes=16, npx=10000)
+    assert launches == {0: 2, 3: 2}, launches
+
+
 def test_c4_800k_sss_frame(bench_gpu, c4_workload):
     """BASELINE config C4: the 800k-triangle knot with the DragonGreen subsurface medium at 1920x1080,
     depth 8, 8 passes in one launch, pixel subset against the oracle."""
