@@ -43,6 +43,12 @@ namespace pt {
 #ifndef PT_ROOT_SKIP
 #define PT_ROOT_SKIP 1
 #endif
+// PT_KEEP_PARKED: lanes parked on a leaf stay parked across a round's end (and a shading batch) instead of
+// the round's last walk step testing their triangles in a forced batch; the next round re-issues their
+// triangle loads (experiment: fewer, fuller triangle batches)
+#ifndef PT_KEEP_PARKED
+#define PT_KEEP_PARKED 0
+#endif
 // PT_DEFER: pass_kernel_u lanes walk on past a passing leaf and test its triangle later (pt_path.h,
 // "deferred leaves"), so triangle batches wait for more lanes without parking them
 #ifndef PT_DEFER
@@ -650,6 +656,10 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         // PF: the parked triangle's geometry, loaded at the park; scoped to the walk loop, which no lane
         // leaves parked (the last step flushes the batch), so it is not live across shading
         float4 pta = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ptb = pta, ptc = pta;
+        constexpr bool KEEP = PT_KEEP_PARKED && PF && !QN && !DEF;
+        if (KEEP && mode == LANE_TRI) {  // parked in an earlier round: its triangle's loads again
+            pta = bload(rt, ptri * 48); ptb = bload(rt, ptri * 48 + 16); ptc = bload(rt, ptri * 48 + 32);
+        }
         for (int k = 0; k < walk_steps; k++) {
             if (k > 0 && !__any(mode == LANE_WALK || mode == LANE_TRI)) break;
             if (PROF) {
@@ -707,7 +717,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             const unsigned long long pend = __ballot(in_batch);
             // PF: no lane leaves the walk loop parked, so the prefetched geometry never lives across shading
             if (pend && (__popcll(pend) >= (unsigned int)tri_min || !__any(mode == LANE_WALK) ||
-                         (PF && k == walk_steps - 1))) {
+                         (PF && !KEEP && k == walk_steps - 1))) {
                 if (PROF) { prof[5]++; prof[6] += (unsigned long long)__popcll(pend); }
                 if (DEF) {
                     if (in_batch) {
