@@ -38,21 +38,10 @@ int pt_scene_upload(pt_context* ctx, int mesh_num, pt_bvh_node_device** bvh_node
                     pt_texture_wrapper* mesh_textures, int texture_num, const pt_configuration* config);
 /* Device bytes of the resident scene and its node / triangle counts. */
 int pt_scene_info(pt_context* ctx, long long* device_bytes, int* node_num, int* triangle_num);
-/* The resident scene's wide BVH records (leaf size 1; 0 when the scene's boxes do not allow them) and
- * whether pass_kernel_u walks them (PT_WIDE, default off: measured slower). */
-int pt_scene_walk_info(pt_context* ctx, int* wide_records, int* wide_walk);
-/* 1: walk the wide records when the scene has them, 0: the binary nodes, -1: PT_WIDE (default 0). */
-int pt_set_wide_walk(pt_context* ctx, int mode);
-/* 1: run the pass as walker waves and shader waves that regroup paths through LDS (pass_kernel_r),
- * 0: every wave walks and shades (pass_kernel_u), -1: PT_REGROUP (default 0). Same results either way. */
-int pt_set_regroup(pt_context* ctx, int mode);
 /* The percentage (1-100, default 100) of the occupancy-sized grid this context's pass launches take:
  * with several contexts rendering frames in flight, the rest of the CUs run the other frames
  * (DESIGN.md §6). Results do not depend on it. */
 int pt_set_grid_share(pt_context* ctx, int percent);
-/* pass_kernel_u's tail pool: once the work is drained, a wave holding at most `paths`
- * paths hands them to wave 0 of its workgroup and ends. 0: off (default), -1: PT_TAIL_POOL. Same results. */
-int pt_set_tail_pool(pt_context* ctx, int paths);
 /* Band order of the work queue. The context's pixels are bands of band_rows rows
  * (pt_set_tiling; one context: bands of the whole frame). pt_band_count gives their number and whether
  * the last is partial; pt_set_band_order(order, n) hands out local band order[i] i-th (a permutation
@@ -72,8 +61,7 @@ const char* pt_last_kernel(pt_context* ctx);
  * build (node_count, the mesh's node count) and that build's transform on the device;
  * pt_mesh_set_transform then re-transforms the mesh's resident triangles and refits its resident node
  * boxes in place by one kernel, without re-uploading the scene: the result equals
- * pt_scene_builder_set_transform's bit for bit. The wide/quantised walks are disabled for a refitted
- * scene (their records are derived from the pre-refit boxes). */
+ * pt_scene_builder_set_transform's bit for bit. */
 int pt_mesh_attach(pt_context* ctx, int mesh, const pt_triangle* local, int tri_start, int tri_count,
                    const pt_bounding_box* init_boxes, int node_count, pt_float3 init_position, pt_float3 init_scale);
 int pt_mesh_set_transform(pt_context* ctx, int mesh, pt_float3 position, pt_float3 scale);

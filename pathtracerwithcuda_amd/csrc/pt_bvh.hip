@@ -208,9 +208,13 @@ __global__ __launch_bounds__(kBlock) void fin_flatten_kernel(FinTree t, pt_bvh_n
                                                              unsigned long long host_leaf_base) {
     const unsigned int k = blockIdx.x * kBlock + threadIdx.x;
     if (k >= t.I + t.L) return;
-    // preorder position: one per ancestor, plus the left sibling's subtree whenever the path turns right
+    // preorder position: one per ancestor, plus the left sibling's subtree whenever the path turns right.
+    // The climb is capped at I + L links: a node on (or below) a cycle never reaches the root, which the
+    // host's size[0] check before this launch rules out; the cap keeps a missed case from hanging the GPU.
     int pos = 0;
+    unsigned int hops = 0;
     for (int c = (int)k; c != 0;) {
+        if (++hops > t.I + t.L) { atomicOr(t.bad, 1); return; }
         const int p = t.parent[c];
         pos += 1;
         if (t.is_right[c]) {
@@ -460,12 +464,22 @@ extern "C" int pt_bvh_build_device(const pt_triangle* tris, int n, int start_ind
         pt_bvh_node_device* d_out = (pt_bvh_node_device*)(base + o_out);
         int* d_slots = (int*)(base + o_slots);
         hipLaunchKernelGGL(fin_up_kernel, dim3(grid_of(L)), dim3(kBlock), 0, stream, ft);
+        BVH_HIP(hipGetLastError());
+        // fin_refs/fin_check count references only: a component holding a cycle (a -> b -> a, each with one
+        // other child) passes them, and its nodes never reach the root. The root's subtree then holds fewer
+        // than I + L nodes: such a tree takes the host finish (its explicit stack visits each node once).
+        int root_size = 0;
+        BVH_HIP(hipMemcpyAsync(&root_size, ft.size, 4, hipMemcpyDeviceToHost, stream));
+        BVH_HIP(hipStreamSynchronize(stream));
+        if (root_size != (int)K) return hipSuccess;  // host finish
         hipLaunchKernelGGL(fin_flatten_kernel, dim3(grid_of((unsigned int)K)), dim3(kBlock), 0, stream, ft, d_out, d_slots,
                            leaf_size, (unsigned long long)(uintptr_t)h_leaf_idx);
         BVH_HIP(hipGetLastError());
         BVH_HIP(hipMemcpyAsync(h_nodes, d_out, N * sizeof(pt_bvh_node_device), hipMemcpyDeviceToHost, stream));
         BVH_HIP(hipMemcpyAsync(h_leaf_idx, d_slots, (size_t)L * leaf_size * sizeof(int), hipMemcpyDeviceToHost, stream));
+        BVH_HIP(hipMemcpyAsync(&bad, ft.bad, 4, hipMemcpyDeviceToHost, stream));
         BVH_HIP(hipStreamSynchronize(stream));
+        if (bad) return hipSuccess;  // host finish
         finished = true;
         return hipSuccess;
     };

@@ -15,20 +15,13 @@
 #define PT_UBLOCK 256
 #endif
 
-// stats[15]: waves of pass_kernel_r that gave up waiting (PT_RG_IDLE_CAP); 0 in every correct run
-#define PT_STAT_RG_CAPPED 15
-
 namespace pt {
 
-// Which pass kernel a render launches (pt_runtime.cpp pass_choice): leaf size 1, instrumented, quantised
-// or wide records, the scene's reachable features; regroup: pass_kernel_r (walker and shader waves)
-// where pass_kernel_u would run on the exact binary nodes; tail_pool > 0: pass_kernel_u with the tail
-// pool, a drained wave holding at most tail_pool paths hands them to wave 0 of its workgroup.
+// Which pass kernel a render launches (pt_runtime.cpp pass_choice): leaf size 1, instrumented, the
+// scene's reachable features (pt_path.h PT_FEAT_*).
 struct PassChoice {
-    bool leaf1, stats, qn, wide;
+    bool leaf1, stats;
     int feat;
-    bool regroup;
-    int tail_pool;
 };
 hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int first_pass, int batch_log2,
                        int write_u8, int grid, int lds_bytes, hipStream_t stream);

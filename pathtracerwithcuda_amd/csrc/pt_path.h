@@ -364,58 +364,6 @@ __device__ __forceinline__ bool mesh_closest(const DevScene& sc, int begin, int 
     return hit;
 }
 
-// The same walk on 16-B quantised nodes (leaf size 1; DESIGN.md §3.1 "quantised nodes"). Each node
-// box is rounded OUTWARD to 16-bit fixed point in its mesh's frame, so it contains the exact box and
-// the walk visits every node the reference visits (plus a few more). A leaf (link < 0) holds its
-// triangle; its skip index is pos + 1. A triangle hit only counts if the reference's own leaf test
-// passes with the exact leaf box and the current min_t — the test every ancestor's exact test
-// implies (box containment, monotone rounding) — so the result is exactly the reference's: the
-// same hits, accepted in the same preorder, under the same min_t. One 16-B load per node instead of
-// two halves the vector-memory instructions, which bound this loop (TA/TD busy).
-__device__ __forceinline__ bool mesh_closest_q(const DevScene& sc, int mesh, int begin, int end, v3 o, v3 d, v3 inv,
-                                               float* ht, float* ht1, float* ht2, int* htri) {
-    const __amdgpu_buffer_rsrc_t rq = make_rsrc(sc.qnodes, sc.node_count * 16);
-    const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
-    const __amdgpu_buffer_rsrc_t rt = make_rsrc(sc.tri_geom, sc.tri_count * 48);
-    const float4* mq = uniform_ptr(sc.mesh_q);
-    const float4 fb = mq[2 * mesh], fs = mq[2 * mesh + 1];
-    float min_t = __builtin_inff();
-    float min_t1 = 0.0f, min_t2 = 0.0f;
-    int min_tri = -1;
-    bool hit = false;
-    int pos = begin;
-    while (pos != end) {
-        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rq, pos * 16, 0, 0);
-        float4 lo, hi;
-        lo.x = fb.x + (float)(q.x & 0xffffu) * fs.x;
-        lo.y = fb.y + (float)(q.x >> 16) * fs.y;
-        lo.z = fb.z + (float)(q.y & 0xffffu) * fs.z;
-        hi.x = fb.x + (float)(q.y >> 16) * fs.x;
-        hi.y = fb.y + (float)(q.z & 0xffffu) * fs.y;
-        hi.z = fb.z + (float)(q.z >> 16) * fs.z;
-        const int link = (int)q.w;
-        float entry;
-        if (box_hit(lo, hi, o, inv, &entry) && entry <= min_t) {
-            if (link < 0) {
-                const int tri = link & 0x7fffffff;
-                float t, t1, t2;
-                float4 a = bload(rt, tri * 48), b = bload(rt, tri * 48 + 16), c = bload(rt, tri * 48 + 32);
-                if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < min_t) {
-                    float ee;
-                    if (box_hit(bload(rn, pos * 32), bload(rn, pos * 32 + 16), o, inv, &ee) && ee <= min_t) {
-                        min_t = t; min_t1 = t1; min_t2 = t2; min_tri = tri; hit = true;
-                    }
-                }
-            }
-            pos++;
-        } else {
-            pos = link < 0 ? pos + 1 : link;
-        }
-    }
-    if (hit) { *ht = min_t; *ht1 = min_t1; *ht2 = min_t2; *htri = min_tri; }
-    return hit;
-}
-
 // The walk of mesh_closest one node at a time, for kernels that interleave walks with shading
 // (pass_kernel_u): the state of one in-flight walk over one mesh, leaf size 1. Same node sequence,
 // same tests, same acceptance rule as mesh_closest<true, false>.
@@ -425,50 +373,13 @@ struct MeshWalk {
     int tri;         // -1 = no hit yet
 };
 
-__device__ __forceinline__ void walk_node(const __amdgpu_buffer_rsrc_t rn, const __amdgpu_buffer_rsrc_t rt, v3 o, v3 d,
-                                          v3 inv, MeshWalk& w) {
-    const float4 lo = bload(rn, w.pos * 32), hi = bload(rn, w.pos * 32 + 16);
-    float entry;
-    if (box_hit(lo, hi, o, inv, &entry) && entry <= w.t) {
-        const int slot = f2i(hi.w);
-        if (slot >= 0) {
-            float t, t1, t2;
-            const float4 a = bload(rt, slot * 48), b = bload(rt, slot * 48 + 16), c = bload(rt, slot * 48 + 32);
-            if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t) {
-                w.t = t; w.t1 = t1; w.t2 = t2; w.tri = slot;
-            }
-        }
-        w.pos++;
-    } else {
-        w.pos = f2i(lo.w);
-    }
-}
-
-// walk_node split at the leaf: the box stage (returns true with the leaf's triangle when the leaf box
-// passes, without advancing) and the triangle stage (tests it, then advances). A lane runs them
-// back to back; between them it may wait while other lanes catch up (pass_kernel_u batches the
-// triangle stage), which changes nothing in its own sequence of tests.
-__device__ __forceinline__ bool walk_box(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri) {
-    const float4 lo = bload(rn, w.pos * 32), hi = bload(rn, w.pos * 32 + 16);
-    float entry;
-    if (box_hit(lo, hi, o, inv, &entry) && entry <= w.t) {
-        const int slot = f2i(hi.w);
-        if (slot >= 0) {
-            tri = slot;
-            return true;
-        }
-        w.pos++;
-    } else {
-        w.pos = f2i(lo.w);
-    }
-    return false;
-}
-
-// walk_box over a run of CHAIN consecutive records loaded together (the node and the next CHAIN - 1 in
-// preorder). A passing internal node's successor is pos + 1 (its left child), whose record is then
-// already in registers, so a descent costs no further dependent load. The visited nodes, their
-// order and every test are walk_box's; only more records are fetched per step (the extra ones beyond
-// a failed test are not used).
+// One step of the stackless preorder walk (path_tracer_kernel.cu:113-150) over a run of CHAIN
+// consecutive records loaded together (the node and the next CHAIN - 1 in preorder). A passing internal
+// node's successor is pos + 1 (its left child), whose record is then already in registers, so a descent
+// costs no further dependent load. The visited nodes, their order and every test are the reference's;
+// only more records are fetched per step (the extra ones beyond a failed test are not used). The walk
+// stops at a leaf whose box passes (returns true with its triangle, not advanced): the lane's triangle
+// test may then wait for a batch (pass_kernel_u), which changes nothing in its own sequence of tests.
 template <int CHAIN>
 struct ChainRecs {
     float4 lo[CHAIN], hi[CHAIN];
@@ -486,9 +397,8 @@ __device__ __forceinline__ void chain_load(const __amdgpu_buffer_rsrc_t rn, int 
 #pragma unroll
     for (int i = 1; i < CHAIN; i++) asm volatile("" ::"v"(r.lo[i].w), "v"(r.hi[i].w));
 }
-// le: the entry of the leaf box that parks the lane (pass_kernel_u's deferred triangle tests)
 template <int CHAIN>
-__device__ __forceinline__ bool chain_test(const ChainRecs<CHAIN>& r, v3 o, v3 inv, MeshWalk& w, int& tri, float& le) {
+__device__ __forceinline__ bool chain_test(const ChainRecs<CHAIN>& r, v3 o, v3 inv, MeshWalk& w, int& tri) {
 #pragma unroll
     for (int i = 0; i < CHAIN; i++) {
         float entry;
@@ -496,7 +406,6 @@ __device__ __forceinline__ bool chain_test(const ChainRecs<CHAIN>& r, v3 o, v3 i
             const int slot = f2i(r.hi[i].w);
             if (slot >= 0) {
                 tri = slot;
-                le = entry;
                 return true;
             }
             w.pos++;
@@ -507,184 +416,18 @@ __device__ __forceinline__ bool chain_test(const ChainRecs<CHAIN>& r, v3 o, v3 i
     }
     return false;
 }
-#ifndef PT_CHAIN_FLAT
-#define PT_CHAIN_FLAT 0
-#endif
-// chain_test for two records without branches (PT_CHAIN_FLAT builds): both boxes are tested, then the
-// outcome of the two-record walk is selected. The second record's test is only USED when the first
-// node is an internal node that passes, exactly when chain_test would run it; the lanes' visited
-// nodes and accepted tests are unchanged.
-__device__ __forceinline__ bool chain_test_flat2(const ChainRecs<2>& r, v3 o, v3 inv, MeshWalk& w, int& tri) {
-    float e0, e1;
-    const bool h0 = box_hit(r.lo[0], r.hi[0], o, inv, &e0) & (e0 <= w.t);
-    const bool h1 = box_hit(r.lo[1], r.hi[1], o, inv, &e1) & (e1 <= w.t);
-    const int s0 = f2i(r.hi[0].w), s1 = f2i(r.hi[1].w);
-    const bool leaf0 = s0 >= 0, leaf1 = s1 >= 0;
-    const bool parked = h0 & (leaf0 | (h1 & leaf1));
-    tri = leaf0 ? s0 : s1;
-    const int skip0 = f2i(r.lo[0].w), skip1 = f2i(r.lo[1].w);
-    w.pos = !h0 ? skip0 : (leaf0 ? w.pos : (!h1 ? skip1 : (leaf1 ? w.pos + 1 : w.pos + 2)));
-    return parked;
-}
-
-template <int CHAIN>
-__device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri,
-                                               float& le) {
-    ChainRecs<CHAIN> r;
-    chain_load<CHAIN>(rn, w.pos, r);
-    if constexpr (CHAIN == 2 && PT_CHAIN_FLAT) return chain_test_flat2(r, o, inv, w, tri);
-    return chain_test<CHAIN>(r, o, inv, w, tri, le);
-}
 template <int CHAIN>
 __device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri) {
-    float le;
-    return walk_box_chain<CHAIN>(rn, o, inv, w, tri, le);
+    ChainRecs<CHAIN> r;
+    chain_load<CHAIN>(rn, w.pos, r);
+    return chain_test<CHAIN>(r, o, inv, w, tri);
 }
 
-// ---- the wide walk (pt_scene.h `wide`, built by pt_runtime.cpp build_wide) ------------------------
-// One step loads a wide record — up to four binary nodes that follow each other in the binary preorder
-// once the levels between them are collapsed — and takes, from the walk's slot on, the first node whose
-// box passes the reference's test (bounding_box.h:83-102 and `entry <= min_t`, path_tracer_kernel.cu:
-// 113-150): an internal node is descended (its record is the next step), a leaf parks the lane for its
-// triangle with the position after it. No passing slot: the record's skip position.
-//
-// Exactness. The reference also tests the collapsed binary nodes; this walk does not. Every box
-// contains its children's boxes (checked on the host), the slab arithmetic (lo - o) * inv, min, max
-// is monotone in the box planes when inv is finite (no 0 * inf), and min_t only decreases: so a node
-// whose test passes would have had every ancestor pass when the reference tested it, with a min_t at
-// least as large. The walk therefore reaches exactly the leaves whose own test passes, in the same
-// preorder, and tests their triangles under the same min_t: the same accepted hits as the reference.
-// A ray with an infinite 1/d (a zero direction component) can produce NaN slabs, for which the
-// argument fails; such lanes walk the binary nodes (pass_kernel_u, begin_segment).
-__device__ __forceinline__ float sel4(float4 v, int j) { return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w)); }
-
-__device__ __forceinline__ bool box_hit_s(float lx, float ly, float lz, float hx, float hy, float hz, v3 o, v3 inv,
-                                          float* entry) {
-    float tx1 = (lx - o.x) * inv.x;
-    float tx2 = (hx - o.x) * inv.x;
-    float ty1 = (ly - o.y) * inv.y;
-    float ty2 = (hy - o.y) * inv.y;
-    float tz1 = (lz - o.z) * inv.z;
-    float tz2 = (hz - o.z) * inv.z;
-    float t_max = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-    float t_min = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-    *entry = t_max;
-    return t_max <= t_min && t_min > 0.0f;
-}
-
-__device__ __forceinline__ bool walk_wide(const __amdgpu_buffer_rsrc_t rw, v3 o, v3 inv, MeshWalk& w, int& tri) {
-    const int rec = w.pos >> 2, k = w.pos & 3;
-    float4 r[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) r[i] = bload(rw, rec * 128 + 16 * i);
-    // all eight loads issued before the first test (one round trip per step)
-#pragma unroll
-    for (int i = 1; i < 8; i++) asm volatile("" ::"v"(r[i].x), "v"(r[i].w));
-    const int skip = f2i(r[7].x), n = f2i(r[7].y);
-    unsigned int pass = 0;
-#pragma unroll
-    for (int j = 0; j < PT_WIDE_SLOTS; j++) {
-        float entry;
-        const bool h = box_hit_s(sel4(r[0], j), sel4(r[2], j), sel4(r[4], j), sel4(r[1], j), sel4(r[3], j),
-                                 sel4(r[5], j), o, inv, &entry);
-        if (h && entry <= w.t && j >= k && j < n) pass |= 1u << j;
-    }
-    if (pass == 0) {
-        w.pos = skip;
-        return false;
-    }
-    const int j = __builtin_ctz(pass);
-    const int ref = f2i(sel4(r[6], j));
-    if (ref > 0) {  // internal: its record is the next step
-        w.pos = ref << 2;
-        return false;
-    }
-    tri = -ref - 1;  // leaf: its triangle, then the next slot (or the skip after the last one)
-    w.pos = j + 1 < n ? ((rec << 2) | (j + 1)) : skip;
-    return true;
-}
-
-// ---- deferred leaves (pass_kernel_u, PT_DEFER) ----------------------------------------------------
-// A lane whose walk reaches a passing leaf need not wait for that leaf's triangle test: it can record
-// the leaf (its triangle and its box entry) and walk on under the min_t it has, which is then at least
-// the reference's. Exactness, for a lane whose 1/d is finite in a scene whose boxes are nested (every
-// node's box contains its children's, DevScene::nested): the slab arithmetic is monotone in the box
-// planes, so a box that passes under some min_t has every ancestor pass under any larger one (the wide
-// walk's argument). Walking under a larger min_t therefore visits every node the reference visits, in
-// the same preorder, plus nodes it would skip; the leaves it reaches are tested later, in preorder, and
-// each counts only if its own test passes under the min_t the reference would have at that leaf
-// (`entry <= min_t`, re-checked when its triangle is tested) — exactly the leaves the reference tests,
-// with the same results. A lane holds one deferred leaf; reaching a second one it parks until the
-// first is resolved, and a mesh walk that ends with a deferred leaf merges only after it is resolved.
-//
-// walk_tri with the triangle's records already loaded. `advance`: the binary walk moves to pos + 1
-// after the leaf; the wide walk already holds the position after it (walk_wide).
-__device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri,
-                                              bool advance = true) {
+// The leaf's triangle test (triangle.h:27-62, accepted when t > 0 && t < min_t, :128) with its records
+// already loaded, then the walk moves past the leaf.
+__device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri) {
     float t, t1, t2;
     if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t) {
-        w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
-    }
-    if (advance) w.pos++;
-}
-
-// walk_tri_geom without advancing, the hit accepted only where `counts` (a deferred leaf whose box still
-// passes under the current min_t, pass_kernel_u's DEF walk): the test runs for every lane of the batch
-__device__ __forceinline__ void walk_tri_geom_if(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri,
-                                                 bool counts) {
-    float t, t1, t2;
-    const bool hit = triangle_test(a, b, c, o, d, &t, &t1, &t2);
-    if (counts && hit && t > 0.0f && t < w.t) {
-        w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
-    }
-}
-
-__device__ __forceinline__ void walk_tri(const __amdgpu_buffer_rsrc_t rt, v3 o, v3 d, MeshWalk& w, int tri,
-                                         bool advance = true) {
-    float t, t1, t2;
-    const float4 a = bload(rt, tri * 48), b = bload(rt, tri * 48 + 16), c = bload(rt, tri * 48 + 32);
-    if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t) {
-        w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
-    }
-    if (advance) w.pos++;
-}
-
-// The same two stages on the 16-B quantised nodes (mesh_closest_q's rules) with the scene-wide frame
-// (fb, fs, wave-uniform): the box stage tests the outward-rounded box; a leaf's triangle then counts
-// only if the reference's own exact leaf test passes too, which walk_tri_q checks with the exact
-// 32-B node loaded alongside the triangle (no extra dependent round trip).
-__device__ __forceinline__ bool walk_box_q(const __amdgpu_buffer_rsrc_t rq, float4 fb, float4 fs, v3 o, v3 inv,
-                                           MeshWalk& w, int& tri) {
-    const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rq, w.pos * 16, 0, 0);
-    float4 lo, hi;
-    lo.x = fb.x + (float)(q.x & 0xffffu) * fs.x;
-    lo.y = fb.y + (float)(q.x >> 16) * fs.y;
-    lo.z = fb.z + (float)(q.y & 0xffffu) * fs.z;
-    hi.x = fb.x + (float)(q.y >> 16) * fs.x;
-    hi.y = fb.y + (float)(q.z & 0xffffu) * fs.y;
-    hi.z = fb.z + (float)(q.z >> 16) * fs.z;
-    const int link = (int)q.w;
-    float entry;
-    if (box_hit(lo, hi, o, inv, &entry) && entry <= w.t) {
-        if (link < 0) {
-            tri = link & 0x7fffffff;
-            return true;
-        }
-        w.pos++;
-    } else {
-        w.pos = link < 0 ? w.pos + 1 : link;
-    }
-    return false;
-}
-
-__device__ __forceinline__ void walk_tri_q(const __amdgpu_buffer_rsrc_t rn, const __amdgpu_buffer_rsrc_t rt, v3 o, v3 d,
-                                           v3 inv, MeshWalk& w, int tri) {
-    float t, t1, t2;
-    const float4 lo = bload(rn, w.pos * 32), hi = bload(rn, w.pos * 32 + 16);
-    const float4 a = bload(rt, tri * 48), b = bload(rt, tri * 48 + 16), c = bload(rt, tri * 48 + 32);
-    float ee;
-    if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t && box_hit(lo, hi, o, inv, &ee) &&
-        ee <= w.t) {
         w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
     }
     w.pos++;
@@ -761,8 +504,7 @@ struct Hit {
     int prim;
 };
 
-// QN: walk the quantised nodes (LEAF1 && !STATS && sc.qnodes, chosen on the host).
-template <bool LEAF1, bool STATS, bool QN>
+template <bool LEAF1, bool STATS>
 __device__ __forceinline__ Hit closest_hit(const DevScene& sc, v3 o, v3 d, Counters* ctr) {
     Hit h;
     h.t = __builtin_inff(); h.t1 = __builtin_inff(); h.t2 = __builtin_inff();
@@ -779,8 +521,7 @@ __device__ __forceinline__ Hit closest_hit(const DevScene& sc, v3 o, v3 d, Count
             const int2 r = uniform_ptr(sc.mesh_range)[m];
             float t, t1, t2;
             int tri;
-            const bool mh = QN ? mesh_closest_q(sc, m, r.x, r.y, o, d, inv, &t, &t1, &t2, &tri)
-                               : mesh_closest<LEAF1, STATS>(sc, r.x, r.y, o, d, inv, &t, &t1, &t2, &tri, ctr);
+            const bool mh = mesh_closest<LEAF1, STATS>(sc, r.x, r.y, o, d, inv, &t, &t1, &t2, &tri, ctr);
             if (mh && t < h.t && t > 0.0f) {
                 h.t = t; h.t1 = t1; h.t2 = t2; h.prim = tri; h.type = 2;
             }
@@ -808,10 +549,10 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
 // One invocation of trace_ray_kernel for one live ray (path_tracer_kernel.cu:381-625).
 // pseed = path_seed(hash(pass), pixel). Returns false when the reference would write -1 into
 // energy_exist_pixels.
-template <bool LEAF1, bool STATS, bool QN>
+template <bool LEAF1, bool STATS>
 __device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
                                            PathState* ps, Counters* ctr) {
-    const Hit h = closest_hit<LEAF1, STATS, QN>(sc, ps->o, ps->d, ctr);
+    const Hit h = closest_hit<LEAF1, STATS>(sc, ps->o, ps->d, ctr);
     return shade_hit<STATS>(sc, cfg, depth, pseed, ps, h, ctr);
 }
 

@@ -61,10 +61,6 @@ inline int f2i_host(float f) { int i; std::memcpy(&i, &f, 4); return i; }
 
 struct SceneStage {
     std::vector<float4> nodes;
-    std::vector<uint4> qnodes;     // empty: quantised walk unavailable (leaf size > 1, odd input)
-    std::vector<float4> mesh_q;
-    std::vector<float4> wide;      // empty: wide walk unavailable (leaf size > 1, a box not inside its parent's)
-    std::vector<int> mesh_wide;    // per mesh: the wide walk's start position, or -1 (no nodes)
     std::vector<int> leaf_tris;
     std::vector<int2> mesh_range;
     std::vector<float4> tri_geom, tri_shade, spheres;
@@ -75,7 +71,7 @@ struct SceneStage {
     int leaf_size = 1;
 };
 
-// 256-bit digest of a translation (the quantised and wide records derive from the rest). Four
+// 256-bit digest of a translation. Four
 // independent 64-bit lanes over interleaved 8-byte words, each a multiply-xorshift chain with its own
 // constants, every array's length mixed in; DevMaterial records are zero-filled before their fields
 // are set, so padding is deterministic. Change detection for the caller's own uploads, not a defence
@@ -149,202 +145,6 @@ DevMaterial to_dev(const pt_material& m) {
     return d;
 }
 
-// 16-bit fixed-point node boxes (pt_scene.h qnodes, pt_path.h mesh_closest_q). The dequantised
-// plane is origin + (float)q * step, evaluated by the device with the same two IEEE operations (no
-// contraction); q is chosen so that the plane lies outside (or on) the exact one, which is all the
-// walk needs for exactness.
-float dequant(float origin, float step, unsigned q) { return origin + (float)q * step; }
-
-unsigned quant_down(float origin, float step, float v) {
-    if (!(step > 0.0f)) return 0;
-    double f = std::floor(((double)v - (double)origin) / (double)step);
-    long long q = f < 0 ? 0 : (f > 65535 ? 65535 : (long long)f);
-    while (q > 0 && dequant(origin, step, (unsigned)q) > v) q--;
-    while (q < 65535 && dequant(origin, step, (unsigned)q + 1) <= v) q++;
-    return (unsigned)q;
-}
-
-unsigned quant_up(float origin, float step, float v) {
-    if (!(step > 0.0f)) return 0;
-    double f = std::ceil(((double)v - (double)origin) / (double)step);
-    long long q = f < 0 ? 0 : (f > 65535 ? 65535 : (long long)f);
-    while (q < 65535 && dequant(origin, step, (unsigned)q) < v) q++;
-    while (q > 0 && dequant(origin, step, (unsigned)q - 1) >= v) q--;
-    return (unsigned)q;
-}
-
-// Builds st.qnodes / st.mesh_q from st.nodes (leaf size 1). Leaves the vectors empty if a node is
-// not representable (non-finite box, a leaf whose skip index is not pos + 1, a box outside the
-// frame); the pass kernel then walks the exact nodes.
-void quantise_nodes(SceneStage& st) {
-    st.qnodes.clear();
-    st.mesh_q.clear();
-    if (st.leaf_size != 1) return;
-    std::vector<uint4> q(st.nodes.size() / 2);
-    // one frame for the whole scene (every mesh_q entry equal), so a walk can hold it in SGPRs
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (size_t i = 0; i < st.nodes.size() / 2; i++) {
-        const float4& a = st.nodes[2 * i];
-        const float4& b = st.nodes[2 * i + 1];
-        const float l[3] = {a.x, a.y, a.z}, h[3] = {b.x, b.y, b.z};
-        for (int k = 0; k < 3; k++) {
-            if (!std::isfinite(l[k]) || !std::isfinite(h[k])) return;
-            lo[k] = std::min(lo[k], l[k]);
-            hi[k] = std::max(hi[k], h[k]);
-        }
-    }
-    float step[3] = {0.0f, 0.0f, 0.0f};
-    for (int k = 0; k < 3; k++) {
-        if (st.nodes.empty() || hi[k] <= lo[k]) continue;
-        step[k] = (float)(((double)hi[k] - (double)lo[k]) / 65534.0);
-        if (!(step[k] > 0.0f)) step[k] = std::numeric_limits<float>::denorm_min();
-        while (dequant(lo[k], step[k], 65535u) < hi[k]) step[k] = std::nextafter(step[k], INFINITY);
-    }
-    for (const int2& r : st.mesh_range) {
-        st.mesh_q.push_back(mkf4(lo[0], lo[1], lo[2], 0.0f));
-        st.mesh_q.push_back(mkf4(step[0], step[1], step[2], 0.0f));
-        for (int i = r.x; i < r.y; i++) {
-            const float4& a = st.nodes[2 * i];
-            const float4& b = st.nodes[2 * i + 1];
-            const float l[3] = {a.x, a.y, a.z}, h[3] = {b.x, b.y, b.z};
-            unsigned ql[3], qh[3];
-            for (int k = 0; k < 3; k++) {
-                ql[k] = quant_down(lo[k], step[k], l[k]);
-                qh[k] = quant_up(lo[k], step[k], h[k]);
-                if (dequant(lo[k], step[k], ql[k]) > l[k] || dequant(lo[k], step[k], qh[k]) < h[k]) return;
-            }
-            const int next = f2i_host(a.w), slot = f2i_host(b.w);
-            uint4 n;
-            n.x = ql[0] | (ql[1] << 16);
-            n.y = ql[2] | (qh[0] << 16);
-            n.z = qh[1] | (qh[2] << 16);
-            if (slot >= 0) {
-                if (next != i + 1) return;
-                n.w = 0x80000000u | (unsigned)slot;
-            } else {
-                n.w = (unsigned)next;
-            }
-            q[i] = n;
-        }
-    }
-    st.qnodes.swap(q);
-}
-
-// Wide records (pt_scene.h `wide`, pt_path.h walk_wide) from the binary preorder nodes of st.nodes, leaf
-// size 1. A wide node stands for a binary internal node B: its slots are B's children, the internal one
-// with the largest box area replaced by its own two children (in place, so the slots stay in the
-// binary preorder) until there are PT_WIDE_SLOTS of them. The walk over them visits the binary
-// preorder without the collapsed levels, which is exact because every box contains its children's
-// (checked here for every parent/child pair; the scene gets no wide records otherwise): see walk_wide.
-void build_wide(SceneStage& st) {
-    st.wide.clear();
-    st.mesh_wide.clear();
-    if (st.leaf_size != 1) return;
-    const int N = (int)(st.nodes.size() / 2);
-    auto lo = [&](int i) { return st.nodes[2 * (size_t)i]; };
-    auto hi = [&](int i) { return st.nodes[2 * (size_t)i + 1]; };
-    auto is_leaf = [&](int i) { return f2i_host(hi(i).w) >= 0; };
-    auto inside = [&](int c, int p) {
-        const float4 a = lo(c), b = hi(c), pa = lo(p), pb = hi(p);
-        return a.x >= pa.x && a.y >= pa.y && a.z >= pa.z && b.x <= pb.x && b.y <= pb.y && b.z <= pb.z;
-    };
-    for (int i = 0; i < N; i++) {  // finite, bounded coordinates: no inf - inf or overflow in (lo - o) * inv
-        const float v[6] = {lo(i).x, lo(i).y, lo(i).z, hi(i).x, hi(i).y, hi(i).z};
-        for (float x : v)
-            if (!(std::fabs(x) < 1e30f)) return;
-    }
-    struct WRec { int n; int bin[PT_WIDE_SLOTS]; int ref[PT_WIDE_SLOTS]; int skip; };
-    std::vector<WRec> recs;
-    std::vector<int> mesh_root;
-    for (const int2& r : st.mesh_range) {
-        if (r.x == r.y) { mesh_root.push_back(-1); continue; }
-        // children of internal node i: i + 1 and the left child's skip index
-        auto left = [&](int i) { return i + 1; };
-        auto right = [&](int i) { return f2i_host(lo(i + 1).w); };
-        for (int i = r.x; i < r.y; i++) {
-            if (is_leaf(i)) {
-                if (f2i_host(lo(i).w) != i + 1) return;
-            } else {
-                if (i + 1 >= r.y || right(i) <= i + 1 || right(i) >= r.y) return;
-                if (!inside(left(i), i) || !inside(right(i), i)) return;
-            }
-        }
-        const int root_id = (int)recs.size();
-        mesh_root.push_back(root_id << 2);
-        // depth-first, numbering a wide node when it is entered: ids in the walk's preorder (a parent
-        // before its children, siblings in slot order)
-        struct Todo { int bin, parent, slot; };
-        std::vector<Todo> todo{{r.x, -1, 0}};
-        while (!todo.empty()) {
-            const Todo t = todo.back();
-            todo.pop_back();
-            const int id = (int)recs.size();
-            recs.push_back(WRec{});
-            if (t.parent >= 0) recs[t.parent].ref[t.slot] = id;
-            const int b = t.bin;
-            int list[PT_WIDE_SLOTS], n = 0;
-            if (is_leaf(b)) {
-                list[n++] = b;  // a one-leaf mesh: its root is the only slot
-            } else {
-                list[n++] = left(b);
-                list[n++] = right(b);
-                while (n < PT_WIDE_SLOTS) {
-                    int best = -1;
-                    float ba = -1.0f;
-                    for (int q = 0; q < n; q++) {
-                        if (is_leaf(list[q])) continue;
-                        const float dx = hi(list[q]).x - lo(list[q]).x, dy = hi(list[q]).y - lo(list[q]).y,
-                                    dz = hi(list[q]).z - lo(list[q]).z;
-                        const float a = dx * dy + dy * dz + dz * dx;
-                        if (a > ba) { ba = a; best = q; }
-                    }
-                    if (best < 0) break;
-                    const int c = list[best];
-                    for (int q = n; q > best + 1; q--) list[q] = list[q - 1];
-                    list[best] = left(c);
-                    list[best + 1] = right(c);
-                    n++;
-                }
-            }
-            recs[id].n = n;
-            for (int q = 0; q < n; q++) {
-                recs[id].bin[q] = list[q];
-                recs[id].ref[q] = is_leaf(list[q]) ? -(f2i_host(hi(list[q]).w) + 1) : 0;
-            }
-            for (int q = n - 1; q >= 0; q--)
-                if (!is_leaf(list[q])) todo.push_back({list[q], id, q});
-        }
-        // skips: after a wide node's subtree, the next slot of its parent, or the parent's own skip
-        recs[root_id].skip = -1;
-        for (int id = root_id; id < (int)recs.size(); id++)
-            for (int s = 0; s < recs[id].n; s++) {
-                const int c = recs[id].ref[s];
-                if (c < 0) continue;
-                recs[c].skip = s + 1 < recs[id].n ? ((id << 2) | (s + 1)) : recs[id].skip;
-            }
-    }
-    // a parent is numbered before its children, so the forward loop above saw every parent's skip first
-    for (size_t id = 0; id < recs.size(); id++)
-        for (int s = 0; s < recs[id].n; s++)
-            if (recs[id].ref[s] >= 0 && recs[id].ref[s] <= (int)id) return;  // not a preorder numbering
-    std::vector<float4> w(recs.size() * 8);
-    for (size_t id = 0; id < recs.size(); id++) {
-        const WRec& R = recs[id];
-        float c[6][PT_WIDE_SLOTS];
-        int ref[PT_WIDE_SLOTS];
-        for (int s = 0; s < PT_WIDE_SLOTS; s++) {
-            const bool used = s < R.n;
-            const float4 a = used ? lo(R.bin[s]) : mkf4(0, 0, 0, 0), b = used ? hi(R.bin[s]) : mkf4(0, 0, 0, 0);
-            c[0][s] = a.x; c[1][s] = b.x; c[2][s] = a.y; c[3][s] = b.y; c[4][s] = a.z; c[5][s] = b.z;
-            ref[s] = used ? R.ref[s] : 0;
-        }
-        for (int k = 0; k < 6; k++) w[id * 8 + k] = mkf4(c[k][0], c[k][1], c[k][2], c[k][3]);
-        w[id * 8 + 6] = mkf4(i2f(ref[0]), i2f(ref[1]), i2f(ref[2]), i2f(ref[3]));
-        w[id * 8 + 7] = mkf4(i2f(R.skip), i2f(R.n), 0.0f, 0.0f);
-    }
-    st.wide.swap(w);
-    st.mesh_wide.swap(mesh_root);
-}
 
 // Reference layout -> device layout (pt_scene.h). Reads every embedded pointer on the host.
 int translate_scene(SceneStage& st, int mesh_num, pt_bvh_node_device** bvh_nodes, pt_triangle* tris, int tri_num,
@@ -488,7 +288,7 @@ struct pt_context {
     void* scene_mem = nullptr;
     size_t scene_bytes = 0;
     DevScene scene{};
-    int node_num = 0, tri_num = 0, wide_num = 0;
+    int node_num = 0, tri_num = 0;
     bool has_scene = false;
     int material_num = 0;
     int scene_feat = PT_FEAT_ALL;  // features the resident scene's materials can reach (pt_path.h PT_FEAT_*)
@@ -508,10 +308,7 @@ struct pt_context {
     LaunchParams* params = nullptr;  // device copy of the launch parameter block
     bool instrumented = false;
     int schedule = -1;  // PT_SCHEDULE_*; -1: environment default (PT_MODE)
-    int wide_mode = -1; // pass_kernel_u walks the wide records: 1 on, 0 off, -1 environment default (PT_WIDE)
-    int regroup_mode = -1;  // pass_kernel_r (walker and shader waves): 1 on, 0 off, -1 environment default (PT_REGROUP)
     int grid_share = 100;   // pt_set_grid_share: percent of the occupancy-sized grid a pass launch takes
-    int tail_pool = -1;     // pt_set_tail_pool: pass_kernel_u's tail pool threshold; 0 off, -1 PT_TAIL_POOL
     // pt_set_band_order / pt_band_cost: the order in which this context's bands are handed out, and
     // per-band ray-segment counters (allocated while measuring); both for the current tiling only
     int* band_order = nullptr;
@@ -520,7 +317,7 @@ struct pt_context {
     unsigned int* band_cost = nullptr;
     int band_cost_n = 0;
     bool band_cost_on = false;
-    int grid[2][2][5][4] = {};
+    int grid[2][2][4] = {};
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
     size_t ev_used = 0;
@@ -555,7 +352,6 @@ struct pt_context {
         ptglm::M4 init_inv{};
     };
     std::unordered_map<int, MeshRefit> refit;
-    bool refitted = false;  // a mesh was refitted: the wide / quantised records are stale
 };
 
 namespace {
@@ -569,7 +365,6 @@ void free_refit(pt_context* ctx) {
     for (auto& kv : ctx->refit)
         if (kv.second.mem) (void)hipFree(kv.second.mem);
     ctx->refit.clear();
-    ctx->refitted = false;
 }
 
 void free_scene(pt_context* ctx) {
@@ -583,8 +378,7 @@ void free_scene(pt_context* ctx) {
 
 // Whether every internal node's box contains both children's boxes, per axis as intervals, in every mesh
 // (preorder records: the left child is n + 1, the right child the left child's skip index when it lies
-// before n's own). pass_kernel_u's deferred triangle tests rest on it (pt_path.h, "deferred leaves"). The
-// reference's builders merge child boxes with min/max, so it holds for their trees; a refit by position
+// before n's own). The reference's builders merge child boxes with min/max, so it holds for their trees; a refit by position
 // and scale (mesh_refit_kernel) maps every corner by the same per-axis monotone function and keeps it.
 int nodes_nested(const std::vector<float4>& nodes, const std::vector<int2>& ranges) {
     auto lo = [&](int n) { return nodes[2 * (size_t)n]; };
@@ -633,10 +427,6 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     size_t i_tex = add(st.tex_desc.data(), st.tex_desc.size() * sizeof(int4));
     size_t i_pool = add(st.tex_pool.data(), st.tex_pool.size());
     size_t i_cube = add(st.cube.data(), st.cube.size());
-    size_t i_q = add(st.qnodes.data(), st.qnodes.size() * sizeof(uint4));
-    size_t i_mq = add(st.mesh_q.data(), st.mesh_q.size() * sizeof(float4));
-    size_t i_w = add(st.wide.data(), st.wide.size() * sizeof(float4));
-    size_t i_mw = add(st.mesh_wide.data(), st.mesh_wide.size() * sizeof(int));
     free_scene(ctx);
     if (total == 0) total = 256;
     PT_HIP(hipMalloc(&ctx->scene_mem, total));
@@ -656,11 +446,6 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     s.tex_desc = (const int4*)(base + pieces[i_tex].off);
     s.tex_pool = (const uint8_t*)(base + pieces[i_pool].off);
     s.cube = (const uint8_t*)(base + pieces[i_cube].off);
-    s.qnodes = st.qnodes.empty() ? nullptr : (const uint4*)(base + pieces[i_q].off);
-    s.mesh_q = st.mesh_q.empty() ? nullptr : (const float4*)(base + pieces[i_mq].off);
-    s.wide = st.wide.empty() ? nullptr : (const float4*)(base + pieces[i_w].off);
-    s.mesh_wide = st.wide.empty() ? nullptr : (const int*)(base + pieces[i_mw].off);
-    s.wide_count = (int)(st.wide.size() / 8);
     s.mesh_num = (int)st.mesh_range.size();
     s.sphere_num = (int)(st.spheres.size() / 2);
     s.leaf_size = st.leaf_size;
@@ -670,17 +455,14 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     s.material_num = (int)st.mats.size();
     s.first_mesh = (int)st.mesh_range.size();
     s.first_range = int2{0, 0};
-    s.first_wide = -1;
     for (size_t m = 0; m < st.mesh_range.size(); m++)
         if (st.mesh_range[m].x != st.mesh_range[m].y) {
             s.first_mesh = (int)m;
             s.first_range = st.mesh_range[m];
-            s.first_wide = st.wide.empty() ? -1 : st.mesh_wide[m];
             break;
         }
     s.nested = nodes_nested(st.nodes, st.mesh_range);
     ctx->node_num = (int)(st.nodes.size() / 2);
-    ctx->wide_num = (int)(st.wide.size() / 8);
     ctx->mesh_range = st.mesh_range;
     ctx->tri_num = (int)(st.tri_geom.size() / 3);
     ctx->material_num = (int)st.mats.size();
@@ -764,39 +546,6 @@ void clear_band_order(pt_context* ctx) {
     ctx->band_cost_on = false;
 }
 
-// PT_QNODES=1 walks the 16-B quantised nodes (bit-identical; measured slower than the exact
-// 32-B walk on MI355X at 1080p, DESIGN.md §3.1, so off by default).
-bool use_qnodes(const pt_context* ctx) {
-    static int on = [] {
-        const char* e = getenv("PT_QNODES");
-        return e && atoi(e) != 0;
-    }();
-    return on && ctx->scene.qnodes != nullptr && !ctx->refitted;
-}
-
-// PT_WIDE=1 makes pass_kernel_u walk the wide records when the scene has them. Off by default: exact,
-// 31% fewer lane walk steps, but each step tests all four slots (the SIMD runs every slot some lane
-// needs) and loads 128 B, so the kernel spends 47% more walk cycles: 7066 vs 9974 Mrays/s on the bench
-// frame (profiles/r02/wide/).
-bool use_wide(const pt_context* ctx) {
-    static int on = [] {
-        const char* e = getenv("PT_WIDE");
-        return e ? atoi(e) != 0 : false;
-    }();
-    const bool want = ctx->wide_mode >= 0 ? ctx->wide_mode != 0 : on;
-    return want && ctx->scene.wide != nullptr && !ctx->refitted && !use_qnodes(ctx);
-}
-
-// PT_REGROUP=1 runs pass_kernel_r (pt_kernels.hip: walker waves and shader waves regrouping paths
-// through LDS) where pass_kernel_u would run.
-bool use_regroup(const pt_context* ctx) {
-    static int on = [] {
-        const char* e = getenv("PT_REGROUP");
-        return e ? atoi(e) != 0 : false;
-    }();
-    return ctx->regroup_mode >= 0 ? ctx->regroup_mode != 0 : on;
-}
-
 // dynamic LDS of pass_kernel_u: every material, then every sphere record (pt_kernels.hip)
 int pass_lds_bytes(const pt_context* ctx) {
     return ctx->material_num * (int)sizeof(DevMaterial) + ctx->scene.sphere_num * 32;
@@ -813,22 +562,16 @@ int render_feat(const pt_context* ctx, const DevConfig& dc) {
 
 // The pass kernel a render of this context launches (pt_kernels.h PassChoice).
 PassChoice pass_choice(const pt_context* ctx, int feat) {
-    static const int env_pool = env_int("PT_TAIL_POOL", 0, 0, 64);
     PassChoice pc;
     pc.leaf1 = ctx->scene.leaf_size == 1;
     pc.stats = ctx->instrumented;
-    pc.qn = use_qnodes(ctx);
-    pc.wide = use_wide(ctx);
     pc.feat = feat;
-    pc.regroup = use_regroup(ctx);
-    pc.tail_pool = ctx->tail_pool >= 0 ? ctx->tail_pool : env_pool;
     return pc;
 }
 
 int pass_grid(pt_context* ctx, int feat) {
     const PassChoice pc = pass_choice(ctx, feat);
-    const int variant = pc.qn ? 1 : (pc.wide ? 2 : (pc.regroup ? 3 : (pc.tail_pool > 0 ? 4 : 0)));
-    int& g = ctx->grid[pc.leaf1 ? 1 : 0][pc.stats ? 1 : 0][variant][feat & 3];
+    int& g = ctx->grid[pc.leaf1 ? 1 : 0][pc.stats ? 1 : 0][feat & 3];
     if (g == 0) {
         g = pass_grid_size(pc, pass_lds_bytes(ctx));
         // PT_GRID_PCT: experiment knob, a percentage of the occupancy-sized grid
@@ -1128,11 +871,9 @@ extern "C" int pt_scene_upload(pt_context* ctx, int mesh_num, pt_bvh_node_device
         if (timing) std::fprintf(stderr, "[pt] scene upload: translate %.2f ms, unchanged (%.2f ms)\n", t_translate, ms());
         return PT_OK;
     }
-    quantise_nodes(*st);
-    build_wide(*st);
     ctx->resident_valid = false;
     rc = upload_stage(ctx, *st);
-    if (timing) std::fprintf(stderr, "[pt] scene upload: translate %.2f ms, quantise+upload -> %.2f ms\n", t_translate, ms());
+    if (timing) std::fprintf(stderr, "[pt] scene upload: translate %.2f ms, upload -> %.2f ms\n", t_translate, ms());
     if (rc != PT_OK) return rc;
     ctx->resident = dg;
     ctx->resident_valid = true;
@@ -1147,27 +888,9 @@ extern "C" int pt_scene_info(pt_context* ctx, long long* bytes, int* node_num, i
     return PT_OK;
 }
 
-extern "C" int pt_set_wide_walk(pt_context* ctx, int mode) {
-    if (!ctx || mode < -1 || mode > 1) { set_error("bad wide walk mode"); return PT_E_ARG; }
-    ctx->wide_mode = mode;
-    return PT_OK;
-}
-
 extern "C" int pt_set_grid_share(pt_context* ctx, int percent) {
     if (!ctx || percent < 1 || percent > 100) { set_error("bad grid share"); return PT_E_ARG; }
     ctx->grid_share = percent;
-    return PT_OK;
-}
-
-extern "C" int pt_set_tail_pool(pt_context* ctx, int paths) {
-    if (!ctx || paths < -1 || paths > 64) { set_error("bad tail pool threshold"); return PT_E_ARG; }
-    ctx->tail_pool = paths;
-    return PT_OK;
-}
-
-extern "C" int pt_set_regroup(pt_context* ctx, int mode) {
-    if (!ctx || mode < -1 || mode > 1) { set_error("bad regroup mode"); return PT_E_ARG; }
-    ctx->regroup_mode = mode;
     return PT_OK;
 }
 
@@ -1228,20 +951,12 @@ extern "C" int pt_mesh_set_transform(pt_context* ctx, int mesh, pt_float3 positi
     PT_HIP(launch_mesh_refit(local, m.tri_start, m.tri_count, init, ctx->mesh_range[mesh].x, m.node_count, T, Tn, C,
                              const_cast<float4*>(ctx->scene.tri_geom), const_cast<float4*>(ctx->scene.tri_shade),
                              const_cast<float4*>(ctx->scene.nodes), ctx->stream));
-    ctx->refitted = true;
     ctx->resident_valid = false;  // the resident scene no longer equals its last upload
     std::memset(ctx->grid, 0, sizeof(ctx->grid));
     return PT_OK;
 }
 
 extern "C" const char* pt_last_kernel(pt_context* ctx) { return ctx ? ctx->last_kernel.c_str() : ""; }
-
-extern "C" int pt_scene_walk_info(pt_context* ctx, int* wide_records, int* wide_walk) {
-    if (!ctx) return PT_E_ARG;
-    if (wide_records) *wide_records = ctx->wide_num;
-    if (wide_walk) *wide_walk = use_wide(ctx) ? 1 : 0;
-    return PT_OK;
-}
 
 extern "C" int pt_frame_setup(pt_context* ctx, int width, int height, void* image_device) {
     if (!ctx || width <= 0 || height <= 0) { set_error("bad frame size"); return PT_E_ARG; }
@@ -1519,6 +1234,7 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
     uint8_t* own256 = ctx->image256;
     if (direct) ctx->image256 = (uint8_t*)image_pixels_256;
     ctx->tiling.band_count = 1;
+    ctx->tiling.band_index = 0;
     const size_t px = (size_t)pixel_count;
     if (!direct && pass_counter != 1) {
         // A pass after the first adds into the CALLER's running sum (path_tracer_kernel.cu:644-651), and

@@ -18,14 +18,6 @@
 //   materials  DevMaterial[M] (96 B), sphere materials appended after mesh materials
 //   textures   int4[K] {width, height, byte offset, -} + one RGBA8 byte pool
 //   cube       RGBA8, 6 faces back to back (x+, x-, y+, y-, z+, z-), length^2 texels each
-//   wide       float4[8*W] wide records (leaf size 1; pt_runtime.cpp build_wide, pt_path.h walk_wide):
-//              {lo.x[0..3]}, {hi.x[0..3]}, {lo.y[..]}, {hi.y[..]}, {lo.z[..]}, {hi.z[..]} of up to
-//              PT_WIDE_SLOTS binary nodes in preorder, {slot refs: >0 wide record, <0 -(triangle + 1)},
-//              {skip position, slot count, -, -}                                          128 B/record
-//              a walk position is record << 2 | slot; -1 = the mesh is done
-//   qnodes     uint4[N] per node, same preorder index as `nodes`: lo.xyz, hi.xyz as u16 fixed point
-//              (value = origin + q * step in the mesh's frame, rounded outward), then a link word:
-//              internal -> next_node_index, leaf -> 0x80000000 | triangle id            16 B/node
 #pragma once
 
 #include <stdint.h>
@@ -72,12 +64,6 @@ struct DevScene {
     const int4* tex_desc;
     const uint8_t* tex_pool;
     const uint8_t* cube;
-    const uint4* qnodes;     // 16-B quantised nodes (leaf size 1), or null: see below
-    const float4* mesh_q;    // per mesh {frame origin}, {frame step} of the quantised nodes
-    const float4* wide;      // wide records (null: the scene walks the binary nodes only)
-    const int* mesh_wide;    // per mesh: the wide walk's start position, -1 when the mesh has no nodes
-    int wide_count;          // records in `wide`
-    int first_wide;          // mesh_wide[first_mesh] (-1 without wide records)
     int mesh_num;
     int sphere_num;
     int leaf_size;
@@ -87,7 +73,7 @@ struct DevScene {
     int material_num;  // records in `materials`
     int first_mesh;    // first mesh with a non-empty node range (mesh_num if none) and that range:
     int2 first_range;  //   where every trace step's mesh walk starts
-    int nested;        // 1: every node's box contains its children's boxes (pass_kernel_u deferred triangles)
+    int nested;        // 1: every node's box contains its children's boxes
 };
 
 // The subset of Core/configuration.h:9-34 that the kernel reads.
@@ -153,7 +139,6 @@ struct DevOutput {
 //              cut into PT_SHARDS regions of seg_cap = ceil(units / PT_SHARDS).
 //   heads      PT_HEAD_SET uints per launch of a pass (extend d: 2d, shade d: 2d + 1), pt_work.h
 #define PT_SHARDS 8
-#define PT_WIDE_SLOTS 4
 struct DevWave {
     float4* q_o[2];
     float4* q_d[2];

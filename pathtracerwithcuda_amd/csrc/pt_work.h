@@ -33,7 +33,8 @@ __device__ __forceinline__ int unit_to_pixel(const DevTiling& til, unsigned int 
         const int band_local = row_local / til.band_rows;
         const int row_in_band = row_local - band_local * til.band_rows;
         const int b = __builtin_nontemporal_load(til.band_order + band_local);
-        return ((b * til.band_count + til.band_index) * til.band_rows + row_in_band) * til.width + x;
+        const int owner = til.band_count > 1 ? til.band_index : 0;  // one owner: band_index is not used (local_bands)
+        return ((b * til.band_count + owner) * til.band_rows + row_in_band) * til.width + x;
     }
     if (til.band_count == 1) return (int)u;
     int row_local = (int)u / til.width;

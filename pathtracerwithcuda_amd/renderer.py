@@ -79,29 +79,9 @@ class Renderer:
         v = self._lib.pt_last_kernel(self._ctx)
         return v.decode() if v else ""
 
-    def walk_info(self) -> dict:
-        """Wide BVH records of the resident scene and whether the pass kernel walks them."""
-        n, on = C.c_int(), C.c_int()
-        check(self._lib.pt_scene_walk_info(self._ctx, C.byref(n), C.byref(on)), "pt_scene_walk_info")
-        return {"wide_records": n.value, "wide_walk": bool(on.value)}
-
-    def set_wide_walk(self, on: bool | None) -> None:
-        """True: walk the wide BVH records when the scene has them; False: the binary nodes; None: PT_WIDE."""
-        check(self._lib.pt_set_wide_walk(self._ctx, -1 if on is None else int(bool(on))), "pt_set_wide_walk")
-
-    def set_regroup(self, on: bool | None) -> None:
-        """True: walker and shader waves regroup paths through LDS (pass_kernel_r); False: every wave walks
-        and shades (pass_kernel_u); None: PT_REGROUP. The image is the same either way."""
-        check(self._lib.pt_set_regroup(self._ctx, -1 if on is None else int(bool(on))), "pt_set_regroup")
-
     def set_grid_share(self, percent: int) -> None:
         """Percentage of the occupancy-sized grid this context's pass launches take (frames in flight)."""
         check(self._lib.pt_set_grid_share(self._ctx, int(percent)), "pt_set_grid_share")
-
-    def set_tail_pool(self, paths: int | None) -> None:
-        """pass_kernel_u's tail pool: a drained wave holding at most `paths` paths hands them to wave 0 of its
-        workgroup (0: off; None: PT_TAIL_POOL). The image is the same either way."""
-        check(self._lib.pt_set_tail_pool(self._ctx, -1 if paths is None else int(paths)), "pt_set_tail_pool")
 
     def band_count(self) -> tuple[int, bool]:
         """(bands of this context's share under its tiling, whether the last one is partial)."""
@@ -199,8 +179,7 @@ class Renderer:
         return dict(zip(keys, (int(x) for x in a)))
 
     def stats_raw(self, n: int = 32) -> list[int]:
-        """The context's raw statistics words (stats[15]: pass_kernel_r waves that gave up waiting, always 0;
-        stats[16..]: PT_UPROF counters)."""
+        """The context's raw statistics words (stats[16..]: PT_UPROF counters)."""
         a = (C.c_ulonglong * n)()
         check(self._lib.pt_stats_all(self._ctx, a, n), "pt_stats_all")
         return [int(x) for x in a]

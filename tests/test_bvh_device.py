@@ -59,10 +59,22 @@ def host_as_bytes(tris, start, leaf_size):
 
 @pytest.mark.parametrize("n,leaf,start,kind", [(1, 1, 0, "rand"), (2, 1, 3, "rand"), (300, 1, 0, "rand"),
                                                (301, 2, 10, "rand"), (1000, 4, 3, "rand"), (257, 3, 0, "rand"),
-                                               (200, 1, 0, "flat"), (120, 1, 0, "dup"), (20000, 1, 7, "rand")])
+                                               (200, 1, 0, "flat"), (120, 1, 0, "dup"), (20000, 1, 7, "rand"),
+                                               (1000, 1, 0, "dup2"), (4096, 1, 0, "same"), (4095, 2, 0, "same"),
+                                               (3000, 1, 0, "dupmix"), (3001, 3, 2, "dupmix")])
 def test_device_builder_equals_host_builder(require_gpu, n, leaf, start, kind):
+    """Equal Morton codes (dup, dup2, same, dupmix) are where the reference's Karras split can give a
+    malformed tree — the ADVICE r02 case: a cycle passes the reference counts, and the device finish
+    must then take the host finish instead of climbing forever (pt_bvh.hip fin_flatten)."""
     if kind == "dup":
         tris = np.repeat(make_tris(3, 1), n // 3, axis=0)
+    elif kind == "dup2":
+        tris = np.repeat(make_tris(2, 5), n // 2, axis=0)
+    elif kind == "same":
+        tris = np.repeat(make_tris(1, 9), n, axis=0)
+    elif kind == "dupmix":  # runs of equal codes between distinct ones
+        base = make_tris(n // 10 + 1, 11)
+        tris = np.concatenate([np.repeat(base[:n // 20 + 1], 5, axis=0), make_tris(n, 13)])[:n]
     else:
         tris = make_tris(n, n * 7 + leaf, kind == "flat")
     tris[:5, 0, 0] = F(-0.0) if n > 5 else tris[:5, 0, 0]  # signed zeros in the folds

@@ -35,23 +35,15 @@ def assert_bitwise(gpu, ref, what=""):
                              f"max |d| {np.nanmax(d):.3g}, mean |d| {np.nanmean(d):.3g}")
 
 
-@pytest.fixture(scope="module", params=["persistent", "persistent_wide", "persistent_regroup", "persistent_tailpool",
-                                        "wavefront"])
+@pytest.fixture(scope="module", params=["persistent", "wavefront"])
 def gpu(require_gpu, request):
-    """Every parity test runs under both kernel schedules (pt_set_schedule), and the persistent one both
-    with its default walk (the binary nodes) and walking the wide BVH records where the scene has them
-    (pt_set_wide_walk, pt_path.h walk_wide), as walker and shader waves (pt_set_regroup,
-    pass_kernel_r) and with the tail pool (pt_set_tail_pool): they must all agree bitwise."""
+    """Every parity test runs under both kernel schedules (pt_set_schedule): the persistent pass kernel
+    and the wavefront queues must both agree bitwise with the oracle. (Round 2's alternative kernels —
+    wide walk, walker/shader regrouping, tail pool — measured slower and were removed from the library;
+    they are kept as patches)"""
     r = pt.Renderer(0)
-    sched = "wavefront" if request.param == "wavefront" else "persistent"
-    r.set_schedule(sched)
-    assert r.schedule() == sched
-    if request.param == "persistent_wide":
-        r.set_wide_walk(True)
-    if request.param == "persistent_regroup":
-        r.set_regroup(True)
-    if request.param == "persistent_tailpool":
-        r.set_tail_pool(32)
+    r.set_schedule(request.param)
+    assert r.schedule() == request.param
     yield r
     r.close()
 
@@ -191,8 +183,7 @@ def test_material_and_config_variants(gpu, variant):
         cfg_kw.update(air_absorption_coef=(0.02, 0.03, 0.05), air_reduced_scattering_coef=(0.05, 0.05, 0.05))
     elif variant == "axis_aligned_rays":
         # no jitter, yaw 0, pitch 0, odd frame: the centre column's primary rays have d.x == 0 and the
-        # centre row's d.y == 0 exactly, so 1/d is infinite there: those lanes take the binary walk
-        # (walk_wide's exactness argument needs a finite 1/d), the others the wide one
+        # centre row's d.y == 0 exactly, so 1/d is infinite there (the slab test meets 0 * inf)
         sc = pt.cornell_scene(pt.torus_knot(50, 14), cube_length=32)
         cfg_kw.update(use_anti_alias=0)
         cam_kw.update(pitch=0.0)
@@ -337,46 +328,6 @@ def test_c5_4k_textured_depth12_frame(bench_gpu):
     assert launches == {0: 1, 3: 1}, launches
 
 
-@pytest.mark.parametrize("variant", ["regroup", "tailpool"])
-@pytest.mark.parametrize("workload", ["metric", "c4", "c5"])
-def test_alternative_kernels_at_the_bench_launch_shape(bench_gpu, c4_workload, workload, variant):
-    """pass_kernel_r (walker waves and shader waves exchanging paths through LDS) and pass_kernel_u with the
-    tail pool, on the bench's launch shape and the C4/C5 configurations: bit-identical to the oracle on a
-    pixel subset and to the default kernel on the whole frame, the same ray-segment count, and no
-    pass_kernel_r wave gave up waiting (stats[15])."""
-    import bench
-    wl = c4_workload if workload == "c4" else bench.Workload(workload)
-    r = bench_gpu
-    r.upload(wl.scene, wl.cfg)
-    r.setup_frame(wl.width, wl.height)
-    r.stats_reset()
-    r.render(wl.cam, wl.cfg, 1, 8, write_u8=2)
-    r.synchronize()
-    base, base8 = r.download()
-    base_segments = r.stats()["segments"]
-    assert r.last_kernel().startswith("pass_kernel_u") and "TAILPOOL" not in r.last_kernel()
-    if variant == "regroup":
-        r.set_regroup(True)
-    else:
-        r.set_tail_pool(32)
-    try:
-        launches, img = _render_workload_subset(r, wl, passes=8, npx=10000, seed=3)
-        if variant == "regroup":
-            assert r.last_kernel().startswith("pass_kernel_r"), r.last_kernel()
-        else:
-            assert "TAILPOOL" in r.last_kernel(), r.last_kernel()
-        raw = r.stats_raw()
-        assert raw[15] == 0, "a pass_kernel_r wave gave up waiting"
-        assert raw[0] == base_segments
-        assert launches == {0: 1, 3: 1}, launches
-        img8 = r.download()[1]
-    finally:
-        r.set_regroup(None)
-        r.set_tail_pool(None)
-    assert np.array_equal(img, base)
-    assert np.array_equal(img8, base8)
-
-
 def test_grid_share_changes_nothing_but_the_grid(bench_gpu):
     """pt_set_grid_share (half the grid per launch, bench.py with three frames in flight): rank 0's
     share of an 8-way tiled metric frame is the same image bit for bit."""
@@ -483,28 +434,6 @@ def test_schedule_switch_on_one_context(require_gpu):
             img, img8, ref, ref8, _ = render_both(r, sc, cam, cfg, passes=4)
             assert_bitwise(img, ref, f"{sched} {w}x{h} float")
             assert_bitwise(img8, ref8, f"{sched} {w}x{h} 8-bit")
-    finally:
-        r.close()
-
-
-def test_bench_scene_has_wide_records(bench_gpu):
-    """The metric scene gets wide BVH records; the pass kernel walks them only when asked (PT_WIDE /
-    pt_set_wide_walk: measured slower)."""
-    import bench
-    wl = bench.Workload("metric")
-    bench_gpu.upload(wl.scene, wl.cfg)
-    info = bench_gpu.walk_info()
-    assert not info["wide_walk"] and info["wide_records"] > 0
-    bench_gpu.set_wide_walk(True)
-    try:
-        assert bench_gpu.walk_info()["wide_walk"]
-    finally:
-        bench_gpu.set_wide_walk(None)
-    leaf3 = pt.cornell_scene(pt.torus_knot(30, 10), cube_length=16, leaf_size=3)
-    r = pt.Renderer(0)
-    try:
-        r.upload(leaf3, pt.configuration(bvh_leaf_node_triangle_num=3))
-        assert r.walk_info() == {"wide_records": 0, "wide_walk": False}  # leaf size 1 only
     finally:
         r.close()
 
@@ -794,9 +723,6 @@ def test_device_refit_equals_the_edited_scene(require_gpu):
             fresh.setup_frame(64, 40)
             fresh.render(cam, cfg, 1, 2, write_u8=2)
             assert np.array_equal(fresh.download()[0], img)
-        r.set_wide_walk(True)
-        assert not r.walk_info()["wide_walk"]  # the wide records predate the refit
-        r.set_wide_walk(None)
         sc.set_rotate(2, (25.0, -40.0, 10.0))
         sc.apply_rotate(2)
         r.upload(sc, cfg)

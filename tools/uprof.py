@@ -1,6 +1,5 @@
 """State-machine occupancy of pass_kernel_u on the benchmark frame (PT_UPROF=1 build of the kernel):
-rounds, walk steps and walking lanes per step, shading / triangle batches and their lanes. With
-PT_REGROUP=1: the walker / shader wave counters of pass_kernel_r."""
+rounds, walk steps and walking lanes per step, shading / triangle batches and their lanes."""
 import ctypes as C
 import json
 import os
@@ -31,28 +30,6 @@ r.synchronize()
 buf = (C.c_ulonglong * 48)()
 pt.lib().pt_stats_all(r._ctx, buf, 48)
 v = list(buf)
-if os.environ.get("PT_REGROUP") == "1":
-    names = ["w_rounds", "handoffs", "lanes_handed", "walk_steps", "walking_lanes", "w_idle_rounds", "shade_batches",
-             "lanes_shaded", "s_idle_rounds", "tri_batches", "cyc_w_handoff", "cyc_w_walk", "cyc_w_idle", "cyc_s_shade",
-             "cyc_s_idle", "tri_lanes"]
-    d = {n: v[16 + i] for i, n in enumerate(names)}
-    d["segments"] = v[0]
-    d["capped"] = v[15]
-    d["kernel"] = r.last_kernel()
-    d["lanes_per_walk_step"] = round(d["walking_lanes"] / max(d["walk_steps"], 1), 2)
-    d["lanes_per_shade_batch"] = round(d["lanes_shaded"] / max(d["shade_batches"], 1), 2)
-    d["lanes_per_tri_batch"] = round(d["tri_lanes"] / max(d["tri_batches"], 1), 2)
-    d["lanes_per_handoff"] = round(d["lanes_handed"] / max(d["handoffs"], 1), 2)
-    wt = d["cyc_w_handoff"] + d["cyc_w_walk"] + d["cyc_w_idle"]
-    for k in ("cyc_w_handoff", "cyc_w_walk", "cyc_w_idle"):
-        d[k.replace("cyc", "frac")] = round(d[k] / max(wt, 1), 3)
-    st = d["cyc_s_shade"] + d["cyc_s_idle"]
-    d["frac_s_idle"] = round(d["cyc_s_idle"] / max(st, 1), 3)
-    d["cyc_per_shade_batch"] = round(d["cyc_s_shade"] / max(d["shade_batches"], 1))
-    d["cyc_per_handoff"] = round(d["cyc_w_handoff"] / max(d["handoffs"], 1))
-    d["cyc_per_walk_step"] = round(d["cyc_w_walk"] / max(d["walk_steps"], 1))
-    print(json.dumps(d))
-    sys.exit(0)
 names = ["rounds", "walk_steps", "walking_lanes", "shade_batches", "lanes_shaded", "tri_batches", "tri_lanes", "refilled",
          "cyc_refill", "cyc_shade", "cyc_walk", "drained_steps_lanes", "parked_lanes", "ready_lanes", "idle_lanes", "cyc_next_segment"]
 d = {n: v[16 + i] for i, n in enumerate(names)}
