@@ -70,7 +70,8 @@ def procedural_texture(w: int, h: int, seed: int) -> np.ndarray:
 
 class Workload:
     """One benchmark workload: scene, configuration, camera and frame size. `metric` is the configuration
-    BASELINE.json's metric is quoted on (the default line); c3-c5 are the heavier BASELINE.json configs
+    BASELINE.json's metric is quoted on (the default line); c2 is BASELINE.json's second config (1280x720,
+    diffuse-only mesh, no spheres); c3-c5 are the heavier BASELINE.json configs
     (1 GPU or tiled), for one-off measurements of the same path at their sizes."""
 
     def __init__(self, name: str):
@@ -84,6 +85,13 @@ class Workload:
             self.key = f"cornell+knot{KNOT[0] * KNOT[1] * 2}_{WIDTH}x{HEIGHT}_spp{SPP}_d{DEPTH}"
             self.desc = ("Cornell box (cornell.obj walls, cube.obj light, iron+glass spheres) + torus knot, "
                          f"{self.scene.triangle_count} triangles, {self.scene.view.sphere_num} spheres")
+            self.data = "synthetic: procedural 70k-triangle torus knot (bunny stand-in) + procedural 512^2 cube map"
+        elif name == "c2":  # Cornell + ~70k-triangle mesh, diffuse only, 1280x720
+            self.width, self.height, self.spp, self.depth = 1280, 720, 8, 8
+            self.scene = pt.cornell_scene(pt.torus_knot(*KNOT), mesh_material="diffuse_white", spheres=False)
+            self.key = f"c2_cornell+knot{KNOT[0] * KNOT[1] * 2}_diffuse_1280x720_spp8_d8"
+            self.desc = ("Cornell box (cornell.obj walls, cube.obj light) + torus knot, diffuse only (specular 0, "
+                         f"n = 1.000293), no spheres, {self.scene.triangle_count} triangles")
             self.data = "synthetic: procedural 70k-triangle torus knot (bunny stand-in) + procedural 512^2 cube map"
         elif name == "c3":  # micro_surface.json: six GGX spheres, skybox, depth of field
             self.width, self.height, self.spp, self.depth = 1920, 1080, 64, 8
@@ -191,7 +199,7 @@ def main() -> int:
     ap.add_argument("--save-image", default="")
     ap.add_argument("--schedule", choices=["persistent", "wavefront"], default=None,
                     help="kernel schedule (default: the library's, PT_MODE)")
-    ap.add_argument("--workload", choices=["metric", "c3", "c4", "c5"], default="metric",
+    ap.add_argument("--workload", choices=["metric", "c2", "c3", "c4", "c5"], default="metric",
                     help="metric: BASELINE.json's metric configuration (default); c3-c5: its heavier configs")
     args = ap.parse_args()
 
@@ -358,6 +366,12 @@ def main() -> int:
     # / the launch's duration measured here with HIP events on the renderer's stream, one frame in flight.
     valu_peak = SIMDS * CLOCK_HZ / 2.0 / 1e9  # G wave-instructions / s
     valu_achieved = valu_insts / avg_launch_s / 1e9 if valu_insts else None
+    # The same instructions over the timed mode's own clock: VALU per frame / ms_per_step (frames in flight
+    # overlap, so this is what the timed figure implies per GPU; it can never exceed 1)
+    valu_timed = valu_insts * launches_per_frame / (ms_per_step / 1000.0) / 1e9 if valu_insts else None
+    # Lane-weighted: a wave-instruction counts active lanes / 64 (PT_UPROF lanes per phase x the PT_DUP VALU
+    # split per phase, tools/lane_weighted.py, recorded in profiles/traffic.json)
+    valu_lanes = float(prof["valu_lane_weighted_per_launch"]) / world if prof.get("valu_lane_weighted_per_launch") else None
     hbm = None
     if traffic is not None:
         hbm_gbs = traffic / avg_launch_s / 1e9
@@ -401,6 +415,9 @@ def main() -> int:
             "traffic": round(traffic) if traffic is not None else None,
             "hbm": hbm,
             "valu_insts_per_launch": round(valu_insts) if valu_insts else None,
+            "frac_timed_mode": round(valu_timed / valu_peak, 4) if valu_timed else None,
+            "frac_lane_weighted": round(valu_lanes / avg_launch_s / 1e9 / valu_peak, 4) if valu_lanes else None,
+            "valu_lane_weighted_per_launch": round(valu_lanes) if valu_lanes else None,
             "kernel": kernel_name,
             "avg_launch_ms": round(avg_launch_s * 1000, 4),
             "avg_launch_source": "HIP events on the renderer stream, one frame in flight",

@@ -298,6 +298,17 @@ def test_metric_frame_at_the_bench_launch_shape(bench_gpu):
     assert launches == {0: 1, 3: 1}, launches
 
 
+def test_c2_diffuse_mesh_frame(bench_gpu):
+    """BASELINE config C2 as its own workload (bench.py --workload c2): the Cornell walls and light with
+    the 70k-triangle mesh, diffuse only, no spheres, 1280x720, 8 passes at the bench launch shape.
+    Pixel subset against the oracle."""
+    import bench
+    wl = bench.Workload("c2")
+    assert (wl.width, wl.height, wl.spp, wl.depth) == (1280, 720, 8, 8) and wl.scene.view.sphere_num == 0
+    launches, _ = _render_workload_subset(bench_gpu, wl, passes=8, npx=20000, seed=2)
+    assert launches == {0: 1, 3: 1}, launches
+
+
 def test_c3_microfacet_sky_dof_frame(bench_gpu):
     """BASELINE config C3: six GGX spheres (roughness 0.01..1, a conductor), the skybox and a thin-lens
     camera at 1920x1080, depth 8. 16 passes run as two batched launches of 8: the second batch's

@@ -1,4 +1,4 @@
-"""State-machine occupancy of pass_kernel_u on the benchmark frame (PT_UPROF=1 build of the kernel):
+"""State-machine occupancy of pass_kernel_u on a benchmark frame (PT_UPROF=1 instance of the kernel):
 rounds, walk steps and walking lanes per step, shading / triangle batches and their lanes."""
 import ctypes as C
 import json
@@ -10,22 +10,22 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 import pathtracerwithcuda_amd as pt  # noqa: E402
 
+# argv[1]: a bench.py workload (default "metric"); one frame of its 8 passes in one launch
+wl = bench.Workload(sys.argv[1] if len(sys.argv) > 1 else "metric")
 r = pt.Renderer(0)
-scene = pt.cornell_scene(pt.torus_knot(*bench.KNOT))
-cfg = pt.configuration(max_tracer_depth=bench.DEPTH)
-cam = pt.camera(bench.WIDTH, bench.HEIGHT, **bench.CAMERA)
+scene, cfg, cam = wl.scene, wl.cfg, wl.cam
 r.upload(scene, cfg)
-r.setup_frame(bench.WIDTH, bench.HEIGHT)
+r.setup_frame(wl.width, wl.height)
 TILE = int(os.environ.get("PT_UPROF_TILE", "1"))  # >1: rank 0's bands of an N-way tiled frame
 if TILE > 1:
     r.set_tiling(bench.BAND_ROWS, TILE, 0)
 SHARE = int(os.environ.get("PT_UPROF_SHARE", "100"))  # percent of the occupancy grid (frames in flight)
 if SHARE != 100:
     r.set_grid_share(SHARE)
-r.render(cam, cfg, 1, bench.SPP, write_u8=2)
+r.render(cam, cfg, 1, 8, write_u8=2)
 r.synchronize()
 r.stats_reset()
-r.render(cam, cfg, 1, bench.SPP, write_u8=2)
+r.render(cam, cfg, 1, 8, write_u8=2)
 r.synchronize()
 buf = (C.c_ulonglong * 48)()
 pt.lib().pt_stats_all(r._ctx, buf, 48)
