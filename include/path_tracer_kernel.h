@@ -22,7 +22,8 @@
  *     pass counter after every scene edit, Core/path_tracer.cpp:101-107) or a pointer changes.
  *   - the per-pixel scratch (not_absorbed / accumulated / rays / energy_exist_pixels /
  *     scatterings) is accepted and ignored: path state lives in registers. memory_allocate
- *     still returns device buffers of the reference sizes.
+ *     still returns buffers of the reference sizes, allocated as the reference allocates them:
+ *     managed memory (hipMallocManaged, host- and device-accessible, path_tracer_kernel.cu:782-796).
  */
 #ifndef PATH_TRACER_KERNEL_H
 #define PATH_TRACER_KERNEL_H

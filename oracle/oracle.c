@@ -261,8 +261,12 @@ static or_v3 on_sphere(int mm, float r1, float r2) {
     return v3(ct, cp * st, sp * st);
 }
 
-/* :238-249 */
+/* :238-249: __powf(E, -a * d); restated as exp(-a * d) (the product and the device compute the same
+ * Cephes exp), except under the CUDA intrinsics model, which follows the reference's __powf(E, .) */
+#define OR_E 2.7182818284590f
 static or_v3 absorption_through(int mm, pt_float3 a, float d) {
+    if (OR_CK(mm))
+        return v3(m_pow(mm, OR_E, -1.0f * a.x * d), m_pow(mm, OR_E, -1.0f * a.y * d), m_pow(mm, OR_E, -1.0f * a.z * d));
     return v3(m_exp(mm, -1.0f * a.x * d), m_exp(mm, -1.0f * a.y * d), m_exp(mm, -1.0f * a.z * d));
 }
 
@@ -382,6 +386,7 @@ static void generate(const or_scene* sc, const pt_render_camera* cam, int rng_ki
                      or_state* st) {
     const pt_configuration* cfg = sc->cfg;
     int mm = sc->math;
+    or_ck_segment(mm, seed, pixel, -1);
     st->alive[k] = k;
     if (st->sig) st->sig[k] = 0;
     st->thr[k] = v3(1.0f, 1.0f, 1.0f);
@@ -428,6 +433,7 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
     int mm = sc->math;
     int k = st->alive[ai];
     int pixel = pixel_of ? pixel_of[k] : k;
+    or_ck_segment(mm, seed, pixel, depth);
     or_v3 o = f3(st->rays[k].origin), d = f3(st->rays[k].direction);
     or_rng rng = rng_seed(rng_kind, mulw(mulw(or_hash(seed), or_hash(pixel)), or_hash(depth)));
 
@@ -542,8 +548,8 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
         st->rays[k].origin = pf3(v_sub(min_point, bias));
         st->rays[k].direction = pf3(refr);
         st->sca[k] = out_sca;
-        float ratio = out_n / in_n;
-        st->thr[k] = v_scale(st->thr[k], ratio * ratio);
+        float ratio = out_n / in_n;  /* :595 __powf(ratio, 2.0f): ratio * ratio, except under the CUDA model */
+        st->thr[k] = v_scale(st->thr[k], OR_CK(mm) ? m_pow(mm, ratio, 2.0f) : ratio * ratio);
     } else {
         st->rad[k] = v_add(st->rad[k], v_mul(st->thr[k], f3(mat.emission_color)));
         st->thr[k] = v_mul(st->thr[k], f3(mat.diffuse_color));
@@ -634,7 +640,10 @@ int or_render_sig(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangl
             or_v3 c = v3(or_clamp(st.rad[k].x, 0.0f, hi), or_clamp(st.rad[k].y, 0.0f, hi), or_clamp(st.rad[k].z, 0.0f, hi));
             if (pass != 1) { img[0] = img[0] + c.x; img[1] = img[1] + c.y; img[2] = img[2] + c.z; }
             else { img[0] = c.x; img[1] = c.y; img[2] = c.z; }
-            if (image256) gamma_u8(math_mode, cfg, img, pass, image256 + (size_t)k * 3);
+            if (image256) {
+                or_ck_segment(math_mode, pass, pixel_list ? pixel_list[k] : k, -2);
+                gamma_u8(math_mode, cfg, img, pass, image256 + (size_t)k * 3);
+            }
             if (sigs) sigs[(size_t)(pass - first_pass) * n + k] = st.sig[k];
         }
     }
@@ -656,12 +665,16 @@ int or_render(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangle* t
  * multi-rank finalize after a reduce). */
 void or_gamma_u8(const pt_configuration* cfg, const float* image, int n, int pass, int math_mode,
                  unsigned char* image256) {
-    for (int k = 0; k < n; k++) gamma_u8(math_mode, cfg, image + (size_t)k * 3, pass, image256 + (size_t)k * 3);
+    for (int k = 0; k < n; k++) {
+        or_ck_segment(math_mode, pass, k, -2);
+        gamma_u8(math_mode, cfg, image + (size_t)k * 3, pass, image256 + (size_t)k * 3);
+    }
 }
 
 /* Math known-answer exports (tests/test_oracle_math.py). */
 void or_math_eval(int which, int math_mode, const float* x, int n, float* out0, float* out1) {
     for (int i = 0; i < n; i++) {
+        or_ck_segment(math_mode, 0, i, 0);
         switch (which) {
             case 0: m_sincos(math_mode, x[i], &out0[i], &out1[i]); break;
             case 1: out0[i] = m_exp(math_mode, x[i]); break;

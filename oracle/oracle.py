@@ -18,7 +18,8 @@ LIB = os.path.join(HERE, "lib", "liboracle.so")
 VARIANTS = {"": LIB, "fma": os.path.join(HERE, "lib", "liboracle_fma.so")}
 
 RNG = {"thrust": 0, "msvc": 1}
-MATH = {"cephes": 0, "libm": 1}
+# "cuda" / "cuda_site": the model of the reference's hardware intrinsics (oracle_math.h), calibration only
+MATH = {"cephes": 0, "libm": 1, "cuda": 2, "cuda_site": 3}
 
 _libs = {}
 

@@ -32,8 +32,15 @@ static inline or_v3 v_cross(or_v3 a, or_v3 b) {                                 
     return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 static inline float v_len(or_v3 a) { return sqrtf(v_dot(a, a)); }                                   /* :1438 */
-/* :1458 — host rsqrtf of cuda_math.hpp:33-36 is 1.0f / sqrtf(x) */
-static inline or_v3 v_norm(or_v3 a) { float inv = 1.0f / sqrtf(v_dot(a, a)); return v_scale(a, inv); }
+/* :1458 — host rsqrtf of cuda_math.hpp:33-36 is 1.0f / sqrtf(x); the device's rsqrtf under the CUDA
+ * model (ck_rsqrt, defined below) */
+static inline float ck_rsqrt(float x);
+static __thread int or_ck_mode;
+static inline or_v3 v_norm(or_v3 a) {
+    float d = v_dot(a, a);
+    float inv = or_ck_mode ? ck_rsqrt(d) : 1.0f / sqrtf(d);
+    return v_scale(a, inv);
+}
 static inline or_v3 v_lerp(or_v3 a, or_v3 b, float t) { return v_add(a, s_scale(t, v_sub(b, a))); } /* :1260 */
 static inline float or_clamp(float f, float a, float b) { return fmaxf(a, fminf(f, b)); }           /* :1290 */
 
@@ -154,28 +161,113 @@ static inline float c_log(float xx) {
     return z;
 }
 
-/* ---- mode dispatch ---- */
+/* ---- a model of the reference CUDA build's hardware intrinsics (tolerance calibration only) ----
+ * OR_MATH_CUDA (2) / OR_MATH_CUDA_SITE (3). The reference calls __sinf, __cosf, __tanf, __expf, __logf
+ * and __powf (path_tracer_kernel.cu:191,203-204,222,235,245-247,344-345,364-365,464,571,595,660-662) and
+ * normalizes with rsqrtf (Math/cuda_math.hpp:1458-1462). Each is modelled as the exact value (double
+ * libm) moved by the maximum error the CUDA C Programming Guide documents for it (intrinsic-function and
+ * single-precision tables), in a direction drawn deterministically:
+ *   __sinf / __cosf  absolute 2^-21.41 / 2^-21.19 on [-pi, pi], scaled by |x| / pi outside ("larger
+ *                    otherwise": the hardware reduces the argument with a fixed-size 2pi)
+ *   __expf           2 + floor(|1.173 x|) ulp
+ *   __logf           absolute 2^-21.41 on [0.5, 2], else 3 ulp
+ *   __powf(x, y)     exp2f(y * __log2f(x)) as the guide derives it: __log2f absolute 2^-22 on [0.5, 2],
+ *                    else 2 ulp; the product rounded to float; the approximate exp2 2 ulp
+ *   __tanf           __sinf(x) * (1 / __cosf(x)), as the guide derives it
+ *   rsqrtf           2 ulp
+ * atanf / asinf / acosf are the accurate CUDA functions there: glibc's (within 1 ulp) stands in.
+ * OR_MATH_CUDA draws the direction from the function and the input bits (the hardware is a deterministic
+ * function of its input: equal inputs in two pixels give equal outputs); OR_MATH_CUDA_SITE draws it from
+ * (pass, pixel, depth, call number within the segment), the per-site model of verdict r02. */
 #define OR_MATH_CEPHES 0
 #define OR_MATH_LIBM 1
+#define OR_MATH_CUDA 2
+#define OR_MATH_CUDA_SITE 3
 
+/* or_ck_mode (declared above v_norm): 0 off, else OR_MATH_CUDA / OR_MATH_CUDA_SITE for this thread */
+static __thread uint64_t or_ck_key;       /* (pass, pixel, depth) of the segment being traced */
+static __thread uint32_t or_ck_calls;     /* intrinsic calls so far in the segment */
+
+static inline uint64_t or_ck_mix(uint64_t x) {
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+/* the segment key: set by the oracle before generate (depth -1) and before each trace step */
+static inline void or_ck_segment(int mode, int pass, int pixel, int depth) {
+    or_ck_mode = (mode == OR_MATH_CUDA || mode == OR_MATH_CUDA_SITE) ? mode : 0;
+    or_ck_key = or_ck_mix(((uint64_t)(uint32_t)pass << 40) ^ ((uint64_t)(uint32_t)pixel << 8) ^ (uint64_t)(uint32_t)(depth + 1));
+    or_ck_calls = 0;
+}
+/* +1 or -1 for a call of function `fn` on input bits `in` */
+static inline int or_ck_sign(int fn, uint32_t in) {
+    uint64_t h;
+    if (or_ck_mode == OR_MATH_CUDA_SITE) h = or_ck_mix(or_ck_key ^ (0x9e3779b97f4a7c15ull * (uint64_t)(++or_ck_calls)));
+    else h = or_ck_mix(((uint64_t)fn << 32) ^ (uint64_t)in ^ 0x632be59bd9b4e019ull);
+    return (h >> 63) ? -1 : 1;
+}
+/* r moved by k ulps in direction s (finite non-zero r only) */
+static inline float or_ck_ulps(float r, int k, int s) {
+    if (!(r == r) || r == 0.0f || isinf(r)) return r;
+    for (int i = 0; i < k; i++) r = nextafterf(r, s > 0 ? INFINITY : -INFINITY);
+    return r;
+}
+static inline void ck_sincos(float x, float* so, float* co) {
+    const double sc = fabs((double)x) > 3.14159265358979 ? fabs((double)x) / 3.14159265358979 : 1.0;
+    *so = (float)(sin((double)x) + or_ck_sign(1, or_f2u(x)) * ldexp(1.0, -21) * pow(2.0, -0.41) * sc);
+    *co = (float)(cos((double)x) + or_ck_sign(2, or_f2u(x)) * ldexp(1.0, -21) * pow(2.0, -0.19) * sc);
+}
+static inline float ck_exp(float x) {  /* __expf */
+    return or_ck_ulps((float)exp((double)x), 2 + (int)floor(fabs(1.173 * (double)x)), or_ck_sign(3, or_f2u(x)));
+}
+static inline float ck_log(float x) {  /* __logf */
+    if (!(x > 0.0f)) return logf(x);
+    if (x >= 0.5f && x <= 2.0f) return (float)(log((double)x) + or_ck_sign(4, or_f2u(x)) * ldexp(1.0, -21) * pow(2.0, -0.41));
+    return or_ck_ulps((float)log((double)x), 3, or_ck_sign(4, or_f2u(x)));
+}
+static inline float ck_log2(float x) {  /* __log2f */
+    if (!(x > 0.0f)) return log2f(x);
+    if (x >= 0.5f && x <= 2.0f) return (float)(log2((double)x) + or_ck_sign(5, or_f2u(x)) * ldexp(1.0, -22));
+    return or_ck_ulps((float)log2((double)x), 2, or_ck_sign(5, or_f2u(x)));
+}
+static inline float ck_exp2(float y) {  /* ex2.approx */
+    return or_ck_ulps((float)exp2((double)y), 2, or_ck_sign(6, or_f2u(y)));
+}
+static inline float ck_pow(float x, float y) {  /* __powf = exp2f(y * __log2f(x)) */
+    if (x == 0.0f) return 0.0f;
+    const float l = ck_log2(x);
+    const float p = y * l;
+    return ck_exp2(p);
+}
+static inline float ck_rsqrt(float x) {  /* rsqrtf */
+    return or_ck_ulps((float)(1.0 / sqrt((double)x)), 2, or_ck_sign(7, or_f2u(x)));
+}
+
+/* ---- mode dispatch ---- */
+
+#define OR_CK(mode) ((mode) == OR_MATH_CUDA || (mode) == OR_MATH_CUDA_SITE)
+#define OR_ACCURATE(mode) ((mode) == OR_MATH_LIBM || OR_CK(mode))
 static inline void m_sincos(int mode, float x, float* s, float* c) {
     if (mode == OR_MATH_LIBM) { *s = sinf(x); *c = cosf(x); }
+    else if (OR_CK(mode)) ck_sincos(x, s, c);
     else c_sincos(x, s, c);
 }
 static inline float m_tan(int mode, float x) {
     if (mode == OR_MATH_LIBM) return tanf(x);
     float s, c;
+    if (OR_CK(mode)) { ck_sincos(x, &s, &c); return s * (1.0f / c); }
     c_sincos(x, &s, &c);
     return s / c;
 }
-static inline float m_atan(int mode, float x) { return mode == OR_MATH_LIBM ? atanf(x) : c_atan(x); }
-static inline float m_asin(int mode, float x) { return mode == OR_MATH_LIBM ? asinf(x) : c_asin(x); }
-static inline float m_acos(int mode, float x) { return mode == OR_MATH_LIBM ? acosf(x) : c_acos(x); }
-static inline float m_exp(int mode, float x) { return mode == OR_MATH_LIBM ? expf(x) : c_exp(x); }
-static inline float m_log(int mode, float x) { return mode == OR_MATH_LIBM ? logf(x) : c_log(x); }
+static inline float m_atan(int mode, float x) { return OR_ACCURATE(mode) ? atanf(x) : c_atan(x); }
+static inline float m_asin(int mode, float x) { return OR_ACCURATE(mode) ? asinf(x) : c_asin(x); }
+static inline float m_acos(int mode, float x) { return OR_ACCURATE(mode) ? acosf(x) : c_acos(x); }
+static inline float m_exp(int mode, float x) { return mode == OR_MATH_LIBM ? expf(x) : (OR_CK(mode) ? ck_exp(x) : c_exp(x)); }
+static inline float m_log(int mode, float x) { return mode == OR_MATH_LIBM ? logf(x) : (OR_CK(mode) ? ck_log(x) : c_log(x)); }
 /* __powf(x, y) for x >= 0 */
 static inline float m_pow(int mode, float x, float y) {
     if (mode == OR_MATH_LIBM) return powf(x, y);
+    if (OR_CK(mode)) return ck_pow(x, y);
     if (x == 0.0f) return 0.0f;
     return c_exp(y * c_log(x));
 }

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
             if (!alive || depth >= cfg.max_depth) {
                 // pixel_256_transform_gamma_corrected_kernel (:644-680) for this (pixel, pass)
                 const v3 c = clamp3(ps.rad, 0.0f, clamp_hi);
-                if (batch_log2 == 0) {
+                if (batch_log2 == 0 && !out.via_rad) {
                     const int pixel = unit_to_pixel(til, unit);
                     float* img = out.image + (size_t)pixel * 3;
                     v3 sum;
@@ -299,7 +299,7 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
                                             int batch_log2, float clamp_hi, int depth) {
     if (til.band_cost) atomicAdd(&til.band_cost[pixel_band(til, unit_to_pixel(til, unit >> batch_log2))], (unsigned int)depth);
     const v3 c = clamp3(ps.rad, 0.0f, clamp_hi);
-    if (batch_log2 == 0) {
+    if (batch_log2 == 0 && !out.via_rad) {
         const int pixel = unit_to_pixel(til, unit);
         float* img = out.image + (size_t)pixel * 3;
         v3 sum;

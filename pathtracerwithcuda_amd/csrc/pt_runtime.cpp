@@ -7,15 +7,18 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <chrono>
 #include <limits>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -122,6 +125,143 @@ StageDigest stage_digest(const SceneStage& a) {
     StageDigest out;
     for (int i = 0; i < 4; i++) out.h[i] = Digester::mix(d.h[i] ^ d.h[(i + 1) & 3], 0xd6e8feb86659fd93ull);
     return out;
+}
+
+// ---- the reference ABI's scene check ---------------------------------------------------------------
+// The reference caller resets pass_counter to 1 after every camera move and every scene edit
+// (Core/path_tracer.cpp:101-107), and a pass-1 call must see in-place edits of the managed scene
+// structures (scene_parser.cpp:645-653 writes materials and spheres in place). Translating the scene to
+// find out whether it changed costs ~5 ms for the metric scene; this digest reads the caller's bytes
+// instead — every byte the translation reads (node arrays, leaf triangle slots, triangles, the materials
+// they point to, spheres, textures, cube-map faces) plus the pointers themselves — in 1-MiB pieces hashed
+// on up to 8 host threads. Equal digest: the resident translation is still the scene.
+struct RawRegion {
+    const void* p;
+    size_t n;
+};
+
+StageDigest digest_regions(const std::vector<RawRegion>& regions) {
+    constexpr size_t kPiece = (size_t)1 << 20;
+    struct Piece { const unsigned char* p; size_t n; };
+    std::vector<Piece> pieces;
+    for (const RawRegion& r : regions) {
+        if (!r.p || r.n == 0) { pieces.push_back({nullptr, 0}); continue; }
+        for (size_t o = 0; o < r.n; o += kPiece)
+            pieces.push_back({(const unsigned char*)r.p + o, r.n - o < kPiece ? r.n - o : kPiece});
+    }
+    std::vector<StageDigest> out(pieces.size());
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (size_t i; (i = next.fetch_add(1)) < pieces.size();) {
+            Digester d;
+            if (pieces[i].p) d.bytes(pieces[i].p, pieces[i].n);
+            else d.word(0, 0x5bd1e995ull);
+            for (int k = 0; k < 4; k++) out[i].h[k] = d.h[k];
+        }
+    };
+    const size_t total = pieces.size();
+    unsigned hw = std::thread::hardware_concurrency();
+    const int threads = (int)std::min<size_t>(std::min<unsigned>(hw ? hw : 1, 8u), (total + 3) / 4);
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(work);
+    work();
+    for (std::thread& t : pool) t.join();
+    Digester all;
+    for (const StageDigest& o : out) all.bytes(o.h, sizeof(o.h));
+    StageDigest r;
+    for (int i = 0; i < 4; i++) r.h[i] = Digester::mix(all.h[i] ^ all.h[(i + 1) & 3], 0xd6e8feb86659fd93ull);
+    return r;
+}
+
+// false when the inputs cannot be read this way (null pointers: the translation reports those)
+bool abi_scene_digest(int mesh_num, pt_bvh_node_device** bvh_nodes, pt_triangle* tris, int sphere_num, pt_sphere* spheres,
+                      pt_cube_map* cube, pt_texture_wrapper* textures, const pt_configuration* cfg, StageDigest* out) {
+    const int leaf_size = cfg->bvh_leaf_node_triangle_num > 0 ? cfg->bvh_leaf_node_triangle_num : 1;
+    if (mesh_num < 0 || sphere_num < 0 || (mesh_num > 0 && (!bvh_nodes || !tris)) || (sphere_num > 0 && !spheres))
+        return false;
+    std::vector<RawRegion> reg;
+    std::vector<long long> head = {mesh_num, sphere_num, leaf_size, (long long)(uintptr_t)bvh_nodes,
+                                   (long long)(uintptr_t)tris, (long long)(uintptr_t)spheres, (long long)(uintptr_t)cube,
+                                   (long long)(uintptr_t)textures};
+    int max_tri = -1;
+    for (int m = 0; m < mesh_num; m++) {
+        const pt_bvh_node_device* nodes = bvh_nodes[m];
+        if (!nodes) return false;
+        const int count = nodes[0].next_node_index;
+        if (count <= 0) return false;
+        head.push_back((long long)(uintptr_t)nodes);
+        head.push_back(count);
+        reg.push_back({nodes, (size_t)count * sizeof(pt_bvh_node_device)});
+        // the leaf slots: one array per mesh in the reference (bvh.cpp:284-287); anything else is read slot by slot
+        const int* lo = nullptr;
+        const int* hi = nullptr;
+        size_t leaves = 0;
+        for (int i = 0; i < count; i++) {
+            const pt_bvh_node_device& n = nodes[i];
+            if (!n.is_leaf || !n.triangle_indices) continue;
+            leaves++;
+            if (!lo || n.triangle_indices < lo) lo = n.triangle_indices;
+            if (!hi || n.triangle_indices > hi) hi = n.triangle_indices;
+        }
+        if (!leaves) continue;
+        const size_t span = (size_t)(hi - lo) + (size_t)leaf_size;
+        if (span <= 2 * leaves * (size_t)leaf_size + 64) {
+            reg.push_back({lo, span * sizeof(int)});
+            for (size_t k = 0; k < span; k++) max_tri = std::max(max_tri, lo[k]);
+        } else {
+            for (int i = 0; i < count; i++) {
+                const pt_bvh_node_device& n = nodes[i];
+                if (!n.is_leaf || !n.triangle_indices) continue;
+                reg.push_back({n.triangle_indices, (size_t)leaf_size * sizeof(int)});
+                for (int k = 0; k < leaf_size; k++) max_tri = std::max(max_tri, n.triangle_indices[k]);
+            }
+        }
+    }
+    const int T = max_tri + 1;
+    head.push_back(T);
+    if (T > 0) reg.push_back({tris, (size_t)T * sizeof(pt_triangle)});
+    // the materials the triangles point to, in first-seen order, then the spheres' (held by value)
+    std::vector<const pt_material*> mats;
+    const pt_material* last = nullptr;
+    int max_tex = -1;
+    for (int t = 0; t < T; t++) {
+        const pt_material* m = tris[t].mat;
+        if (m == last) continue;
+        last = m;
+        if (!m) return false;
+        if (std::find(mats.begin(), mats.end(), m) == mats.end()) mats.push_back(m);
+    }
+    for (const pt_material* m : mats) {
+        reg.push_back({m, sizeof(pt_material)});
+        max_tex = std::max(max_tex, std::max(m->diffuse_texture_id, m->specular_texture_id));
+    }
+    if (sphere_num > 0) reg.push_back({spheres, (size_t)sphere_num * sizeof(pt_sphere)});
+    for (int k = 0; k < sphere_num; k++)
+        max_tex = std::max(max_tex, std::max(spheres[k].mat.diffuse_texture_id, spheres[k].mat.specular_texture_id));
+    head.push_back(max_tex);
+    if (max_tex >= 0) {
+        if (!textures) return false;
+        reg.push_back({textures, (size_t)(max_tex + 1) * sizeof(pt_texture_wrapper)});
+        for (int k = 0; k <= max_tex; k++) {
+            const pt_texture_wrapper& tw = textures[k];
+            if (tw.width <= 0 || tw.height <= 0 || !tw.pixels) return false;
+            reg.push_back({tw.pixels, (size_t)tw.width * tw.height * 4});
+        }
+    }
+    if (cube) {
+        reg.push_back({cube, sizeof(pt_cube_map)});
+        if (cube->length > 0) {
+            const unsigned char* faces[6] = {cube->m_x_positive_map, cube->m_x_negative_map, cube->m_y_positive_map,
+                                             cube->m_y_negative_map, cube->m_z_positive_map, cube->m_z_negative_map};
+            for (const unsigned char* f : faces) {
+                if (!f) return false;
+                reg.push_back({f, (size_t)cube->length * cube->length * 4});
+            }
+        }
+    }
+    reg.insert(reg.begin(), RawRegion{head.data(), head.size() * sizeof(long long)});
+    *out = digest_regions(reg);
+    return true;
 }
 
 DevMaterial to_dev(const pt_material& m) {
@@ -343,6 +483,16 @@ struct pt_context {
     // A digest, not a host copy, so a context holds no second copy of the scene on the host.
     bool resident_valid = false;
     StageDigest resident{};
+    // the reference ABI's scene check: digest of the caller's raw scene bytes at the last translation
+    bool raw_valid = false;
+    StageDigest raw{};
+    // the reference ABI on host-visible images: one-pass launches go through pass_rad (rad_single) and the
+    // accumulate launch waits for the caller's running sum, uploaded on copy_stream meanwhile (acc_wait)
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t copy_done = nullptr;
+    bool rad_single = false;
+    hipEvent_t acc_wait = nullptr;
+    std::function<int()> before_acc;  // run once the pass kernel is enqueued, before the accumulate waits
     std::vector<int2> mesh_range;  // node range per mesh of the resident scene
     // pt_mesh_attach: per mesh, device copies of its mesh-local triangles (v0..v2, n0..n2 as float4) and
     // initial node corners, and the inverse of the transform of those boxes
@@ -705,6 +855,16 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         ctx->mat_air_n_valid = true;
     }
     if (ctx->schedule == PT_SCHEDULE_WAVEFRONT || (ctx->schedule < 0 && use_wavefront())) {
+        if (ctx->before_acc) {
+            const std::function<int()> f = std::move(ctx->before_acc);
+            ctx->before_acc = nullptr;
+            const int rc = f();
+            if (rc != PT_OK) return rc;
+        }
+        if (ctx->acc_wait) {  // finalize_kernel adds into the running sum: it must have arrived
+            PT_HIP(hipStreamWaitEvent(ctx->stream, ctx->acc_wait, 0));
+            ctx->acc_wait = nullptr;
+        }
         int rc = ensure_wave(ctx, ctx->tiling.unit_count, D);
         if (rc != PT_OK) return rc;
         lp.wave = ctx->wave;
@@ -738,7 +898,8 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     const int units = ctx->tiling.unit_count;
     int most = 1;
     while (most * 2 <= max_pass_batch() && (long long)units * most * 2 <= (1ll << 28)) most *= 2;
-    if (most > 1 && pass_count > 1) {
+    const bool rad1 = ctx->rad_single;  // one-pass launches write pass_rad and are accumulated afterwards
+    if ((most > 1 && pass_count > 1) || rad1) {
         const size_t need = (size_t)units * (size_t)most * 12;
         if (need > ctx->pass_rad_bytes) {
             if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
@@ -749,6 +910,7 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         }
     }
     lp.out.pass_rad = ctx->pass_rad;
+    lp.out.via_rad = rad1 ? 1 : 0;
     PT_HIP(hipMemcpyAsync(ctx->params, &lp, sizeof(lp), hipMemcpyHostToDevice, ctx->stream));
     for (int i = 0; i < pass_count;) {
         int b = 1, lg = 0;
@@ -762,7 +924,16 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         if (rc != PT_OK) return rc;
         PT_HIP(launch_pass(ctx->params, pc, first, lg, w8, g, pass_lds_bytes(ctx), ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
-        if (lg > 0) {
+        if (lg > 0 || rad1) {
+            if (ctx->before_acc) {
+                const std::function<int()> f = std::move(ctx->before_acc);
+                ctx->before_acc = nullptr;
+                if ((rc = f()) != PT_OK) return rc;
+            }
+            if (ctx->acc_wait) {  // the running sum this accumulate adds into is still being uploaded
+                PT_HIP(hipStreamWaitEvent(ctx->stream, ctx->acc_wait, 0));
+                ctx->acc_wait = nullptr;
+            }
             if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;
             PT_HIP(launch_accumulate(ctx->params, units, first, lg, w8, ctx->stream));
             if ((rc = ev_end(ctx)) != PT_OK) return rc;
@@ -821,6 +992,8 @@ extern "C" int pt_context_create(int device, pt_context** out) {
     ctx->device = device;
     int rc = ensure_device(ctx);
     if (rc == PT_OK && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { set_error("stream"); rc = PT_E_HIP; }
+    if (rc == PT_OK && hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess) { set_error("stream"); rc = PT_E_HIP; }
+    if (rc == PT_OK && hipEventCreateWithFlags(&ctx->copy_done, hipEventDisableTiming) != hipSuccess) { set_error("event"); rc = PT_E_HIP; }
     if (rc == PT_OK && hipMalloc(&ctx->fetch, PT_HEAD_SET * sizeof(unsigned int)) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
     if (rc == PT_OK && hipMalloc(&ctx->stats, PT_STATS_BYTES) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
     if (rc == PT_OK && hipMalloc(&ctx->params, sizeof(LaunchParams)) != hipSuccess) { set_error("alloc"); rc = PT_E_HIP; }
@@ -834,6 +1007,7 @@ extern "C" void pt_context_destroy(pt_context* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
     free_scene(ctx);
     if (ctx->own_image && ctx->image) (void)hipFree(ctx->image);
     if (ctx->image256) (void)hipFree(ctx->image256);
@@ -849,6 +1023,8 @@ extern "C" void pt_context_destroy(pt_context* ctx) {
     for (auto e : ctx->ev_start) (void)hipEventDestroy(e);
     for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+    if (ctx->copy_done) (void)hipEventDestroy(ctx->copy_done);
     delete ctx;
 }
 
@@ -859,6 +1035,7 @@ extern "C" int pt_scene_upload(pt_context* ctx, int mesh_num, pt_bvh_node_device
     int rc = ensure_device(ctx);
     if (rc != PT_OK) return rc;
     static const bool timing = getenv("PT_UPLOAD_TIMING") != nullptr;
+    ctx->raw_valid = false;  // the reference ABI sets it again when it is the caller
     const auto t0 = std::chrono::steady_clock::now();
     auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
     std::unique_ptr<SceneStage> st(new SceneStage());
@@ -952,6 +1129,7 @@ extern "C" int pt_mesh_set_transform(pt_context* ctx, int mesh, pt_float3 positi
                              const_cast<float4*>(ctx->scene.tri_geom), const_cast<float4*>(ctx->scene.tri_shade),
                              const_cast<float4*>(ctx->scene.nodes), ctx->stream));
     ctx->resident_valid = false;  // the resident scene no longer equals its last upload
+    ctx->raw_valid = false;
     std::memset(ctx->grid, 0, sizeof(ctx->grid));
     return PT_OK;
 }
@@ -1200,6 +1378,9 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
                                    pt_texture_wrapper* mesh_textures_device, pt_configuration* config_device) {
     (void)not_absorbed_colors_device; (void)accumulated_colors_device; (void)rays_device;
     (void)energy_exist_pixels_device; (void)scatterings_device;
+    static const bool timing = getenv("PT_ABI_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
     pt_context* ctx = default_context();
     if (!ctx) { report("path_tracer_kernel: context"); return; }
     if (!config_device || !render_camera_device || pixel_count <= 0) {
@@ -1209,18 +1390,6 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
     }
     const pt_configuration config = *config_device;  // host read, as :706
     const pt_render_camera cam = *render_camera_device;
-    const void* key[6] = {bvh_nodes_device, triangles_device, spheres_device, sky_cube_map_device, mesh_textures_device,
-                          nullptr};
-    bool same = ctx->has_scene && ctx->key_counts[0] == mesh_num && ctx->key_counts[1] == sphere_num;
-    for (int i = 0; i < 5 && same; i++) same = ctx->key[i] == key[i];
-    if (!same || pass_counter == 1) {
-        int rc = pt_scene_upload(ctx, mesh_num, bvh_nodes_device, triangles_device, -1, sphere_num, spheres_device,
-                                 sky_cube_map_device, mesh_textures_device, -1, &config);
-        if (rc != PT_OK) { report("path_tracer_kernel: scene"); return; }
-        for (int i = 0; i < 6; i++) ctx->key[i] = key[i];
-        ctx->key_counts[0] = mesh_num;
-        ctx->key_counts[1] = sphere_num;
-    }
     const int width = (int)cam.resolution.x;
     if (width <= 0 || pixel_count % width != 0) {
         set_error("[Hip]Error pixel_count %d is not a multiple of the camera width %d", pixel_count, width);
@@ -1228,6 +1397,14 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
         return;
     }
     const int height = pixel_count / width;
+    if (hipSetDevice(ctx->device) != hipSuccess) { set_error("[Hip]Error set device"); report("path_tracer_kernel"); return; }
+    // Image memory. Device memory is rendered in place. Host-visible memory (host, or managed as the
+    // reference allocates it, Core/image.cpp:15-27) is mirrored in HBM: on this pool a kernel reaches
+    // managed memory at ~20 GB/s but the copy engines at ~55 GB/s (profiles/r03/abi/managed_probe.txt).
+    // A continuation pass adds into the CALLER's running sum (path_tracer_kernel.cu:644-651), which the
+    // caller may have advanced on the host in between (Core/path_tracer.cpp:46-91 switches per pass to the
+    // CPU twin on the same buffers): it is uploaded on the copy stream while the pass kernel runs (the
+    // pass writes pass_rad; accumulate_kernel waits for the upload and adds the pass into the mirror).
     const bool direct = is_device_memory(image_pixels) && is_device_memory(image_pixels_256);
     int rc = ensure_image(ctx, width, height, direct ? (void*)image_pixels : nullptr);
     if (rc != PT_OK) { report("path_tracer_kernel: image"); return; }
@@ -1237,16 +1414,56 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
     ctx->tiling.band_index = 0;
     const size_t px = (size_t)pixel_count;
     if (!direct && pass_counter != 1) {
-        // A pass after the first adds into the CALLER's running sum (path_tracer_kernel.cu:644-651), and
-        // the caller may have advanced it on the host in between: Core/path_tracer.cpp:46-91 switches
-        // between this entry and the CPU twin path_tracer_cpu per pass on the same (managed) buffers.
-        // So the mirror is refreshed from the caller's buffer before every continuation pass.
-        if (hipMemcpyAsync(ctx->image, image_pixels, px * 12, hipMemcpyDefault, ctx->stream) != hipSuccess) {
-            set_error("[Hip]Error uploading the caller's running sum");
-            rc = PT_E_HIP;
+        // enqueued by render_passes right after the pass kernel (a copy from pageable memory can hold the
+        // host until it is done, so it must not come before the launch)
+        ctx->before_acc = [ctx, image_pixels, px]() -> int {
+            hipError_t e = hipMemcpyAsync(ctx->image, image_pixels, px * 12, hipMemcpyDefault, ctx->copy_stream);
+            if (e == hipSuccess) e = hipEventRecord(ctx->copy_done, ctx->copy_stream);
+            if (e != hipSuccess) { set_error("[Hip]Error uploading the caller's running sum"); return PT_E_HIP; }
+            ctx->acc_wait = ctx->copy_done;
+            return PT_OK;
+        };
+    }
+    const double t_image = ms();
+    // The scene: re-read when a pointer changes or on pass 1 (the reference caller resets the pass
+    // counter after every edit and camera move, Core/path_tracer.cpp:101-107); translated and uploaded only
+    // when the caller's bytes changed (abi_scene_digest).
+    double t_digest = 0.0;
+    bool uploaded = false;
+    const void* key[6] = {bvh_nodes_device, triangles_device, spheres_device, sky_cube_map_device, mesh_textures_device,
+                          nullptr};
+    bool same = ctx->has_scene && ctx->key_counts[0] == mesh_num && ctx->key_counts[1] == sphere_num;
+    for (int i = 0; i < 5 && same; i++) same = ctx->key[i] == key[i];
+    if (rc == PT_OK && (!same || pass_counter == 1)) {
+        StageDigest rd;
+        const bool rd_ok = abi_scene_digest(mesh_num, bvh_nodes_device, triangles_device, sphere_num, spheres_device,
+                                            sky_cube_map_device, mesh_textures_device, &config, &rd);
+        t_digest = ms() - t_image;
+        if (!(same && rd_ok && ctx->raw_valid && ctx->raw == rd)) {
+            rc = pt_scene_upload(ctx, mesh_num, bvh_nodes_device, triangles_device, -1, sphere_num, spheres_device,
+                                 sky_cube_map_device, mesh_textures_device, -1, &config);
+            uploaded = true;
+            if (rc == PT_OK) {
+                for (int i = 0; i < 6; i++) ctx->key[i] = key[i];
+                ctx->key_counts[0] = mesh_num;
+                ctx->key_counts[1] = sphere_num;
+                ctx->raw = rd;
+                ctx->raw_valid = rd_ok;
+            } else {
+                report("path_tracer_kernel: scene");
+            }
         }
     }
+    const double t_scene = ms();
+    ctx->rad_single = !direct;
     if (rc == PT_OK) rc = render_passes(ctx, &cam, &config, pass_counter, 1, 1);
+    ctx->rad_single = false;
+    ctx->before_acc = nullptr;
+    if (ctx->acc_wait) {  // not consumed (an error before the accumulate launch): order it anyway
+        (void)hipStreamWaitEvent(ctx->stream, ctx->acc_wait, 0);
+        ctx->acc_wait = nullptr;
+    }
+    const double t_launch = ms();
     if (rc == PT_OK) {
         if (!direct) {
             hipError_t e = hipMemcpyAsync(image_pixels, ctx->image, px * 12, hipMemcpyDefault, ctx->stream);
@@ -1257,8 +1474,14 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
             set_error("[Hip]Error synchronize");
             rc = PT_E_HIP;
         }
+    } else {
+        (void)hipStreamSynchronize(ctx->stream);
     }
     if (direct) { ctx->image256 = own256; ctx->image = nullptr; ctx->image_cap = 0; ctx->own_image = false; }
+    if (timing)
+        std::fprintf(stderr, "[pt] path_tracer_kernel pass %d: image %.3f, digest %.3f, scene %.3f%s, launch %.3f, "
+                     "render+copy+sync %.3f, total %.3f ms\n", pass_counter, t_image, t_digest, t_scene - t_image - t_digest,
+                     uploaded ? " (uploaded)" : "", t_launch - t_scene, ms() - t_launch, ms());
     if (rc != PT_OK) report("path_tracer_kernel");
 }
 

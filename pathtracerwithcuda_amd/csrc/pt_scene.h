@@ -128,6 +128,8 @@ struct DevOutput {
     unsigned int* fetch;     // PT_HEAD_SET work heads of the single-kernel pass (zeroed before launch)
     unsigned long long* stats;  // [0] ray segments, [1..] optional instrumentation
     float* pass_rad;         // batched passes: clamped radiance per (unit, pass) (12 B), summed in order
+    int via_rad;             // 1: one-pass launches write pass_rad too (accumulate_kernel adds them afterwards)
+    int pad;
 };
 
 // Wavefront queues (pt_wavefront.hip). Ray slots are dense per depth; path state is per pixel.

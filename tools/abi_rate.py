@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """PCIe-inclusive rate of the drop-in reference ABI on the bench frame: the 8 passes
-of the 1920x1080 metric frame through `path_tracer_kernel` with host image buffers, one call per
-pass as Core/path_tracer.cpp:40-67 makes them (each call ends with the running sum and the 8-bit
-image copied back to the host, like the reference's managed memory seen from the host). The scene
-is the bench scene; the first frame (scene translation and upload) is excluded.
+of the 1920x1080 metric frame through `path_tracer_kernel`, one call per pass as
+Core/path_tracer.cpp:40-67 makes them, on image buffers allocated as the reference allocates them
+(--image managed: hipMallocManaged, Core/image.cpp:15-27) or as pageable host arrays (--image host).
+Each call ends with the running sum and the 8-bit image in the caller's buffers. The scene is the
+bench scene; the first frame (scene translation and upload) is excluded; every frame's pass 1 re-checks
+the scene (the reference resets pass_counter after a camera move).
 
-    python tools/abi_rate.py [--frames F]
+    python tools/abi_rate.py [--frames F] [--image managed|host]
 """
 import argparse
 import ctypes as C
@@ -24,12 +26,24 @@ import pathtracerwithcuda_amd as pt  # noqa: E402
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--image", choices=["managed", "host"], default="managed")
     args = ap.parse_args()
     wl = bench.Workload("metric")
     v, cam, cfg = wl.scene.view, wl.cam, wl.cfg
     n = wl.width * wl.height
-    img = (pt._abi.Float3 * n)()
-    img8 = (pt._abi.UChar3 * n)()
+    hip = None
+    if args.image == "managed":
+        hip = C.CDLL("libamdhip64.so")
+        hip.hipMallocManaged.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+        hip.hipFree.argtypes = [C.c_void_p]
+        pimg, pimg8 = C.c_void_p(), C.c_void_p()
+        assert hip.hipMallocManaged(C.byref(pimg), n * 12, 1) == 0
+        assert hip.hipMallocManaged(C.byref(pimg8), n * 3, 1) == 0
+        img = C.cast(pimg, C.POINTER(pt._abi.Float3))
+        img8 = C.cast(pimg8, C.POINTER(pt._abi.UChar3))
+    else:
+        img = (pt._abi.Float3 * n)()
+        img8 = (pt._abi.UChar3 * n)()
     scratch = [C.c_void_p() for _ in range(5)]
     lib = pt.lib()
     lib.path_tracer_kernel_memory_allocate(*[C.byref(s) for s in scratch], n)
@@ -50,6 +64,9 @@ def main() -> None:
         frame()
     dt = (time.perf_counter() - t0) / args.frames
     lib.path_tracer_kernel_memory_free(*scratch)
+    if hip is not None:
+        hip.hipFree(pimg)
+        hip.hipFree(pimg8)
     r = pt.Renderer(0)  # segments of one frame (identical for every frame: fact 2 of SURVEY.md)
     r.upload(wl.scene, wl.cfg)
     r.setup_frame(wl.width, wl.height)
@@ -58,7 +75,7 @@ def main() -> None:
     r.synchronize()
     seg = r.stats()["segments"]
     r.close()
-    print(json.dumps({"path": "path_tracer_kernel (reference ABI, host image buffers, one call per pass)",
+    print(json.dumps({"path": f"path_tracer_kernel (reference ABI, {args.image} image buffers, one call per pass)",
                       "ms_per_frame": round(dt * 1000, 3), "mrays_per_s": round(seg / dt / 1e6, 1),
                       "ms_per_pass": [round(x / args.frames * 1000, 3) for x in per_pass[1:]],
                       "segments_per_frame": seg, "frames": args.frames}), flush=True)
