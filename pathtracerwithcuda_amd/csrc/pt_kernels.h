@@ -27,6 +27,8 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
                        int write_u8, int grid, int lds_bytes, hipStream_t stream);
 hipError_t launch_accumulate(const LaunchParams* params_dev, int units, int first_pass, int batch_log2, int write_u8,
                              hipStream_t stream);
+hipError_t launch_accumulate_one(const LaunchParams* params_dev, int unit_begin, int unit_end, int pass, int batch_log2,
+                                 int j, int write_u8, const float* rad, hipStream_t stream);
 hipError_t launch_extend(const LaunchParams* P, bool gen, bool leaf1, bool stats, int depth, int pass, hipStream_t s);
 hipError_t launch_shade(const LaunchParams* P, bool first, bool last, bool stats, int depth, int pass, hipStream_t s);
 int shade_grid_waves();

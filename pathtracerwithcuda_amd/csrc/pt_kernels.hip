@@ -588,6 +588,33 @@ __global__ __launch_bounds__(PT_BLOCK) void accumulate_kernel(const LaunchParams
         store_u8(P->cfg, sum, first_pass + batch - 1, P->out.image256 + (size_t)pixel * 3);
 }
 
+// One pass of a batched launch added into the running sum: pass `pass` is slot j of every unit's run of
+// 2^batch_log2 pass radiances in rad (path_tracer_kernel.cu:644-651 for that pass), then its 8-bit output.
+// The reference ABI's pass cache (pt_runtime.cpp abi_render_pass) serves one pass per call this way.
+__global__ __launch_bounds__(PT_BLOCK) void accumulate_one_kernel(const LaunchParams* __restrict__ P, int pass,
+                                                                  int batch_log2, int j, int write_u8,
+                                                                  const float* __restrict__ rad, int unit_begin,
+                                                                  int unit_end) {
+    const unsigned int lu = unit_begin + blockIdx.x * PT_BLOCK + threadIdx.x;
+    if (lu >= (unsigned int)unit_end) return;
+    const int pixel = unit_to_pixel(P->til, lu);
+    float* img = P->out.image + (size_t)pixel * 3;
+    const float* pr = rad + (((size_t)lu << batch_log2) + (size_t)j) * 3;
+    const v3 c = mk3(pr[0], pr[1], pr[2]);
+    const v3 sum = pass == 1 ? c : mk3(img[0], img[1], img[2]) + c;
+    img[0] = sum.x; img[1] = sum.y; img[2] = sum.z;
+    if (write_u8 && P->out.image256) store_u8(P->cfg, sum, pass, P->out.image256 + (size_t)pixel * 3);
+}
+
+hipError_t launch_accumulate_one(const LaunchParams* params_dev, int unit_begin, int unit_end, int pass, int batch_log2,
+                                 int j, int write_u8, const float* rad, hipStream_t stream) {
+    const int units = unit_end - unit_begin;
+    if (units <= 0) return hipSuccess;
+    hipLaunchKernelGGL(accumulate_one_kernel, dim3((units + PT_BLOCK - 1) / PT_BLOCK), dim3(PT_BLOCK), 0, stream,
+                       params_dev, pass, batch_log2, j, write_u8, rad, unit_begin, unit_end);
+    return hipGetLastError();
+}
+
 // Gamma/8-bit from a float running sum (used after a multi-GPU reduce, and by the reference
 // ABI when the caller asks for the 8-bit image only at the end of a frame).
 __global__ __launch_bounds__(PT_BLOCK) void u8_kernel(DevConfig cfg, const float* image, uint8_t* image256,

@@ -493,6 +493,18 @@ struct pt_context {
     bool rad_single = false;
     hipEvent_t acc_wait = nullptr;
     std::function<int()> before_acc;  // run once the pass kernel is enqueued, before the accumulate waits
+    // the reference ABI's pass cache (abi_render_pass): two batched launches ("slots") of the camera /
+    // configuration in spec_cam / spec_cfg, slot s holding passes [spec_first[s], spec_first[s] + count)
+    bool spec_valid = false;
+    int spec_first[2] = {0, 0}, spec_count = 0, spec_lg = 0, spec_w = 0, spec_h = 0;
+    pt_render_camera spec_cam{};
+    pt_configuration spec_cfg{};
+    float* spec_rad[2] = {nullptr, nullptr};
+    size_t spec_rad_bytes[2] = {0, 0};
+    LaunchParams* spec_params[2] = {nullptr, nullptr};  // each slot's launch parameters (device)
+    hipEvent_t spec_done[2] = {nullptr, nullptr};
+    hipStream_t acc_stream = nullptr;  // the ABI's per-call accumulate and download
+    hipEvent_t chunk_up[4] = {nullptr, nullptr, nullptr, nullptr};  // the running sum's upload, per chunk
     std::vector<int2> mesh_range;  // node range per mesh of the resident scene
     // pt_mesh_attach: per mesh, device copies of its mesh-local triangles (v0..v2, n0..n2 as float4) and
     // initial node corners, and the inverse of the transform of those boxes
@@ -558,6 +570,7 @@ int nodes_nested(const std::vector<float4>& nodes, const std::vector<int2>& rang
 }
 
 int upload_stage(pt_context* ctx, const SceneStage& st) {
+    ctx->spec_valid = false;
     struct Piece { const void* src; size_t bytes; size_t off; };
     std::vector<Piece> pieces;
     size_t total = 0;
@@ -822,8 +835,9 @@ bool use_wavefront() {
     return w != 0;
 }
 
-int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config, int first_pass,
-                  int pass_count, int write_u8) {
+// The launch parameter block of a render call (without pass_rad), plus the per-material shading constants
+// for the configured air index when they are stale.
+int prepare_launch(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config, LaunchParams& lp) {
     if (!ctx->has_scene) { set_error("no scene uploaded"); return PT_E_STATE; }
     if (!ctx->image) { set_error("no frame set up"); return PT_E_STATE; }
     if (!cam || !config) { set_error("null camera/config"); return PT_E_ARG; }
@@ -836,7 +850,7 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     out.image256 = ctx->image256;
     out.fetch = ctx->fetch;
     out.stats = ctx->stats;
-    LaunchParams lp;
+    lp = LaunchParams{};
     lp.sc = ctx->scene;
     lp.cfg = dc;
     lp.cam = dcam;
@@ -847,14 +861,27 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
                                                                                                        : nullptr;
     lp.til.band_cost = ctx->band_cost_on && ctx->band_cost_n == nb ? ctx->band_cost : nullptr;
     lp.out = out;
-    const int D = dc.max_depth > 0 ? dc.max_depth : 0;
     if (!ctx->mat_air_n_valid || ctx->mat_air_n != dc.air_n) {  // DevMaterial shading constants
         PT_HIP(launch_material_consts(const_cast<DevMaterial*>(ctx->scene.materials), ctx->material_num, dc.air_n,
                                       ctx->stream));
         ctx->mat_air_n = dc.air_n;
         ctx->mat_air_n_valid = true;
     }
-    if (ctx->schedule == PT_SCHEDULE_WAVEFRONT || (ctx->schedule < 0 && use_wavefront())) {
+    return PT_OK;
+}
+
+bool wavefront_schedule(const pt_context* ctx) {
+    return ctx->schedule == PT_SCHEDULE_WAVEFRONT || (ctx->schedule < 0 && use_wavefront());
+}
+
+int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config, int first_pass,
+                  int pass_count, int write_u8) {
+    LaunchParams lp;
+    int prc = prepare_launch(ctx, cam, config, lp);
+    if (prc != PT_OK) return prc;
+    const DevConfig& dc = lp.cfg;
+    const int D = dc.max_depth > 0 ? dc.max_depth : 0;
+    if (wavefront_schedule(ctx)) {
         if (ctx->before_acc) {
             const std::function<int()> f = std::move(ctx->before_acc);
             ctx->before_acc = nullptr;
@@ -943,6 +970,124 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     return PT_OK;
 }
 
+// ---- the reference ABI's pass cache ------------------------------------------------------------------
+// The reference caller renders a frame as consecutive calls with pass_counter 1, 2, 3, ... on the same
+// scene, camera and configuration until the user moves (Core/path_tracer.cpp:40-67, window.cpp:194-215).
+// A one-pass launch costs far more than a pass of a batched launch: it lasts as long as its longest path
+// (2.1 ms for a 1920x1080 pass against 0.86 ms per pass of an 8-pass launch). So a call
+// whose pass is not cached renders passes [pass, pass + B) (B = max_pass_batch()) as two batched launches
+// of B/2 passes each into two radiance buffers ("slots"; pass_kernel batch_log2 > 0) and adds only its
+// own pass into the running sum, as soon as the first launch is done; the second runs on while the calls
+// that follow take their passes from the first slot (the caller's copies then overlap GPU work). Each
+// call adds its pass with accumulate_one_kernel on acc_stream, after that slot's launch. Every draw is
+// keyed by (pass, pixel, depth) (path_tracer_kernel.cu:324,415), so a pass rendered ahead is bit-identical
+// to one rendered on demand. The cache holds for the camera and configuration bytes it was rendered with
+// and the resident scene (any upload or refit drops it); the scene itself is re-checked on
+// pass_counter == 1 as before. PT_ABI_PASS_CACHE=0 turns it off. *done: the stream the result is on.
+// The caller's image buffers of a reference-ABI call: device memory (rendered in place) or host-visible
+// (mirrored in HBM: the running sum uploaded before, the result downloaded after).
+struct AbiImage {
+    pt_float3* img;
+    pt_uchar3* img8;
+    bool direct;
+    bool pageable;  // not registered with HIP: a copy holds the host thread, so chunking cannot overlap
+};
+
+int abi_render_pass(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config, int pass,
+                    const AbiImage& io, hipStream_t* done, bool* downloaded) {
+    static const int on = env_int("PT_ABI_PASS_CACHE", 1, 0, 1);
+    const int B = max_pass_batch();
+    *done = ctx->stream;
+    *downloaded = false;
+    if (!on || B < 4 || wavefront_schedule(ctx) || ctx->instrumented) return render_passes(ctx, cam, config, pass, 1, 1);
+    ctx->before_acc = nullptr;  // this path moves the running sum itself, in chunks (below)
+    if (!ctx->acc_stream) PT_HIP(hipStreamCreateWithFlags(&ctx->acc_stream, hipStreamNonBlocking));
+    for (hipEvent_t& e : ctx->chunk_up)
+        if (!e) PT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (int k = 0; k < 2; k++) {
+        if (!ctx->spec_done[k]) PT_HIP(hipEventCreateWithFlags(&ctx->spec_done[k], hipEventDisableTiming));
+        if (!ctx->spec_params[k]) PT_HIP(hipMalloc(&ctx->spec_params[k], sizeof(LaunchParams)));
+    }
+    LaunchParams lp;
+    int rc = prepare_launch(ctx, cam, config, lp);
+    if (rc != PT_OK) return rc;
+    const bool key = ctx->spec_valid && ctx->spec_w == ctx->width && ctx->spec_h == ctx->height &&
+                     std::memcmp(&ctx->spec_cam, cam, sizeof(*cam)) == 0 &&
+                     std::memcmp(&ctx->spec_cfg, config, sizeof(*config)) == 0;
+    int slot = -1;
+    for (int k = 0; k < 2 && key; k++)
+        if (pass >= ctx->spec_first[k] && pass < ctx->spec_first[k] + ctx->spec_count) slot = k;
+    const int units = ctx->tiling.unit_count;
+    if (slot < 0) {
+        int lg = 0;
+        while ((2 << lg) <= B / 2 && ((long long)units << (lg + 1)) <= (1ll << 28)) lg++;
+        const int feat = render_feat(ctx, lp.cfg);
+        const PassChoice pc = pass_choice(ctx, feat);
+        ctx->last_kernel = pass_kernel_desc(pc, pass_lds_bytes(ctx));
+        const size_t need = (size_t)units * ((size_t)1 << lg) * 12;
+        for (int k = 0; k < 2; k++) {
+            if (need > ctx->spec_rad_bytes[k]) {
+                PT_HIP(hipStreamSynchronize(ctx->stream));  // an earlier launch may still write the old buffer
+                if (ctx->spec_rad[k]) (void)hipFree(ctx->spec_rad[k]);
+                ctx->spec_rad[k] = nullptr;
+                ctx->spec_rad_bytes[k] = 0;
+                PT_HIP(hipMalloc(&ctx->spec_rad[k], need));
+                ctx->spec_rad_bytes[k] = need;
+            }
+            LaunchParams ls = lp;
+            ls.out.pass_rad = ctx->spec_rad[k];
+            ls.out.via_rad = 0;
+            const int first = pass + k * (1 << lg);
+            PT_HIP(hipMemcpyAsync(ctx->spec_params[k], &ls, sizeof(ls), hipMemcpyHostToDevice, ctx->stream));
+            PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
+            if ((rc = ev_begin(ctx, 0)) != PT_OK) return rc;
+            // the second slot leaves an eighth of the workgroup slots free: the calls it overlaps launch their
+            // accumulates meanwhile, which would otherwise wait for its persistent workgroups to end
+            const int g = pass_grid(ctx, feat);
+            PT_HIP(launch_pass(ctx->spec_params[k], pc, first, lg, 0, k == 0 ? g : std::max(1, g - g / 8),
+                               pass_lds_bytes(ctx), ctx->stream));
+            if ((rc = ev_end(ctx)) != PT_OK) return rc;
+            PT_HIP(hipEventRecord(ctx->spec_done[k], ctx->stream));
+            ctx->spec_first[k] = first;
+        }
+        ctx->spec_valid = true;
+        ctx->spec_count = 1 << lg;
+        ctx->spec_lg = lg;
+        ctx->spec_w = ctx->width;
+        ctx->spec_h = ctx->height;
+        ctx->spec_cam = *cam;
+        ctx->spec_cfg = *config;
+        slot = 0;
+    }
+    // The pass added into the running sum on acc_stream once its slot's launch is done. A host-visible image
+    // moves in four chunks of pixels: chunk c's running sum goes up on copy_stream while chunk c - 1's result
+    // comes down on acc_stream (the link is full duplex: 1.06 -> ~0.7 ms per call for 1920x1080).
+    hipStream_t as = ctx->acc_stream;
+    PT_HIP(hipStreamWaitEvent(as, ctx->spec_done[slot], 0));
+    // the accumulate's parameters: ctx->params on this stream (the slots' launches read their own blocks)
+    PT_HIP(hipMemcpyAsync(ctx->params, &lp, sizeof(lp), hipMemcpyHostToDevice, as));
+    const int K = io.direct || io.pageable ? 1 : 4;
+    const bool up = !io.direct && pass != 1;  // pass 1 overwrites: nothing to add into
+    for (int c = 0; c < K; c++) {
+        const int b0 = (int)((long long)units * c / K), b1 = (int)((long long)units * (c + 1) / K);
+        if (up) {
+            PT_HIP(hipMemcpyAsync(ctx->image + (size_t)b0 * 3, io.img + b0, (size_t)(b1 - b0) * 12, hipMemcpyDefault,
+                                  ctx->copy_stream));
+            PT_HIP(hipEventRecord(ctx->chunk_up[c], ctx->copy_stream));
+            PT_HIP(hipStreamWaitEvent(as, ctx->chunk_up[c], 0));
+        }
+        PT_HIP(launch_accumulate_one(ctx->params, b0, b1, pass, ctx->spec_lg, pass - ctx->spec_first[slot], 1,
+                                     ctx->spec_rad[slot], as));
+        if (!io.direct) {
+            PT_HIP(hipMemcpyAsync(io.img + b0, ctx->image + (size_t)b0 * 3, (size_t)(b1 - b0) * 12, hipMemcpyDefault, as));
+            PT_HIP(hipMemcpyAsync(io.img8 + b0, ctx->image256 + (size_t)b0 * 3, (size_t)(b1 - b0) * 3, hipMemcpyDefault, as));
+        }
+    }
+    *downloaded = !io.direct;
+    *done = as;
+    return PT_OK;
+}
+
 std::mutex g_default_mutex;
 pt_context* g_default = nullptr;
 
@@ -958,6 +1103,17 @@ pt_context* default_context() {
 
 void report(const char* where) {
     std::fprintf(stderr, "%s (%s)\n", g_last_error.c_str(), where);
+}
+
+// Host memory HIP does not know (plain malloc / ctypes arrays): copies from it are staged and synchronous.
+bool is_pageable(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return true;
+    }
+    return attr.type == hipMemoryTypeUnregistered;
 }
 
 bool is_device_memory(const void* p) {
@@ -1008,6 +1164,7 @@ extern "C" void pt_context_destroy(pt_context* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
+    if (ctx->acc_stream) (void)hipStreamSynchronize(ctx->acc_stream);
     free_scene(ctx);
     if (ctx->own_image && ctx->image) (void)hipFree(ctx->image);
     if (ctx->image256) (void)hipFree(ctx->image256);
@@ -1016,6 +1173,13 @@ extern "C" void pt_context_destroy(pt_context* ctx) {
     if (ctx->params) (void)hipFree(ctx->params);
     if (ctx->wave_mem) (void)hipFree(ctx->wave_mem);
     if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
+    for (int k = 0; k < 2; k++) {
+        if (ctx->spec_rad[k]) (void)hipFree(ctx->spec_rad[k]);
+        if (ctx->spec_params[k]) (void)hipFree(ctx->spec_params[k]);
+        if (ctx->spec_done[k]) (void)hipEventDestroy(ctx->spec_done[k]);
+    }
+    for (hipEvent_t e : ctx->chunk_up)
+        if (e) (void)hipEventDestroy(e);
     clear_band_order(ctx);
     if (ctx->shrink_buf) (void)hipFree(ctx->shrink_buf);
     if (ctx->shrink_tiles) (void)hipFree(ctx->shrink_tiles);
@@ -1024,6 +1188,7 @@ extern "C" void pt_context_destroy(pt_context* ctx) {
     for (auto e : ctx->ev_stop) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+    if (ctx->acc_stream) (void)hipStreamDestroy(ctx->acc_stream);
     if (ctx->copy_done) (void)hipEventDestroy(ctx->copy_done);
     delete ctx;
 }
@@ -1130,6 +1295,7 @@ extern "C" int pt_mesh_set_transform(pt_context* ctx, int mesh, pt_float3 positi
                              const_cast<float4*>(ctx->scene.nodes), ctx->stream));
     ctx->resident_valid = false;  // the resident scene no longer equals its last upload
     ctx->raw_valid = false;
+    ctx->spec_valid = false;
     std::memset(ctx->grid, 0, sizeof(ctx->grid));
     return PT_OK;
 }
@@ -1434,54 +1600,81 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
                           nullptr};
     bool same = ctx->has_scene && ctx->key_counts[0] == mesh_num && ctx->key_counts[1] == sphere_num;
     for (int i = 0; i < 5 && same; i++) same = ctx->key[i] == key[i];
-    if (rc == PT_OK && (!same || pass_counter == 1)) {
-        StageDigest rd;
-        const bool rd_ok = abi_scene_digest(mesh_num, bvh_nodes_device, triangles_device, sphere_num, spheres_device,
-                                            sky_cube_map_device, mesh_textures_device, &config, &rd);
-        t_digest = ms() - t_image;
-        if (!(same && rd_ok && ctx->raw_valid && ctx->raw == rd)) {
-            rc = pt_scene_upload(ctx, mesh_num, bvh_nodes_device, triangles_device, -1, sphere_num, spheres_device,
-                                 sky_cube_map_device, mesh_textures_device, -1, &config);
-            uploaded = true;
-            if (rc == PT_OK) {
-                for (int i = 0; i < 6; i++) ctx->key[i] = key[i];
-                ctx->key_counts[0] = mesh_num;
-                ctx->key_counts[1] = sphere_num;
-                ctx->raw = rd;
-                ctx->raw_valid = rd_ok;
-            } else {
-                report("path_tracer_kernel: scene");
-            }
+    auto upload = [&](const StageDigest& rd, bool rd_ok) {
+        rc = pt_scene_upload(ctx, mesh_num, bvh_nodes_device, triangles_device, -1, sphere_num, spheres_device,
+                             sky_cube_map_device, mesh_textures_device, -1, &config);
+        uploaded = true;
+        ctx->spec_valid = false;
+        if (rc == PT_OK) {
+            for (int i = 0; i < 6; i++) ctx->key[i] = key[i];
+            ctx->key_counts[0] = mesh_num;
+            ctx->key_counts[1] = sphere_num;
+            ctx->raw = rd;
+            ctx->raw_valid = rd_ok;
+        } else {
+            report("path_tracer_kernel: scene");
         }
+    };
+    StageDigest rd;
+    bool rd_ok = false;
+    if (rc == PT_OK && !same) {  // new pointers: translate before rendering
+        rd_ok = abi_scene_digest(mesh_num, bvh_nodes_device, triangles_device, sphere_num, spheres_device,
+                                 sky_cube_map_device, mesh_textures_device, &config, &rd);
+        t_digest = ms() - t_image;
+        upload(rd, rd_ok);
     }
     const double t_scene = ms();
-    ctx->rad_single = !direct;
-    if (rc == PT_OK) rc = render_passes(ctx, &cam, &config, pass_counter, 1, 1);
-    ctx->rad_single = false;
-    ctx->before_acc = nullptr;
-    if (ctx->acc_wait) {  // not consumed (an error before the accumulate launch): order it anyway
-        (void)hipStreamWaitEvent(ctx->stream, ctx->acc_wait, 0);
-        ctx->acc_wait = nullptr;
+    // Same pointers on pass 1: render with the resident scene and digest the caller's bytes while the GPU
+    // works; if they changed after all, the render is redone on the new scene (pass 1 overwrites the sum).
+    const bool check_after = rc == PT_OK && same && pass_counter == 1;
+    hipStream_t done = ctx->stream;
+    bool downloaded = false;
+    const AbiImage io{image_pixels, image_pixels_256, direct, !direct && is_pageable(image_pixels)};
+    auto render = [&]() {
+        ctx->rad_single = !direct;
+        if (rc == PT_OK) rc = abi_render_pass(ctx, &cam, &config, pass_counter, io, &done, &downloaded);
+        ctx->rad_single = false;
+        ctx->before_acc = nullptr;
+        if (ctx->acc_wait) {  // not consumed (an error before the accumulate launch): order it anyway
+            (void)hipStreamWaitEvent(done, ctx->acc_wait, 0);
+            ctx->acc_wait = nullptr;
+        }
+    };
+    render();
+    if (check_after) {
+        const double t0d = ms();
+        rd_ok = abi_scene_digest(mesh_num, bvh_nodes_device, triangles_device, sphere_num, spheres_device,
+                                 sky_cube_map_device, mesh_textures_device, &config, &rd);
+        t_digest = ms() - t0d;
+        if (!(rd_ok && ctx->raw_valid && ctx->raw == rd)) {
+            (void)hipStreamSynchronize(done);
+            (void)hipStreamSynchronize(ctx->stream);
+            upload(rd, rd_ok);
+            render();
+        }
     }
     const double t_launch = ms();
     if (rc == PT_OK) {
-        if (!direct) {
-            hipError_t e = hipMemcpyAsync(image_pixels, ctx->image, px * 12, hipMemcpyDefault, ctx->stream);
-            if (e == hipSuccess) e = hipMemcpyAsync(image_pixels_256, ctx->image256, px * 3, hipMemcpyDefault, ctx->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (!direct && downloaded) {
+            if (hipStreamSynchronize(done) != hipSuccess) { set_error("[Hip]Error synchronize"); rc = PT_E_HIP; }
+        } else if (!direct) {
+            hipError_t e = hipMemcpyAsync(image_pixels, ctx->image, px * 12, hipMemcpyDefault, done);
+            if (e == hipSuccess) e = hipMemcpyAsync(image_pixels_256, ctx->image256, px * 3, hipMemcpyDefault, done);
+            if (e == hipSuccess) e = hipStreamSynchronize(done);
             if (e != hipSuccess) { set_error("[Hip]Error %s downloading the image", hipGetErrorString(e)); rc = PT_E_HIP; }
-        } else if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
+        } else if (hipStreamSynchronize(done) != hipSuccess) {
             set_error("[Hip]Error synchronize");
             rc = PT_E_HIP;
         }
     } else {
+        (void)hipStreamSynchronize(done);
         (void)hipStreamSynchronize(ctx->stream);
     }
     if (direct) { ctx->image256 = own256; ctx->image = nullptr; ctx->image_cap = 0; ctx->own_image = false; }
     if (timing)
-        std::fprintf(stderr, "[pt] path_tracer_kernel pass %d: image %.3f, digest %.3f, scene %.3f%s, launch %.3f, "
-                     "render+copy+sync %.3f, total %.3f ms\n", pass_counter, t_image, t_digest, t_scene - t_image - t_digest,
-                     uploaded ? " (uploaded)" : "", t_launch - t_scene, ms() - t_launch, ms());
+        std::fprintf(stderr, "[pt] path_tracer_kernel pass %d: image %.3f, scene %.3f%s, launch + digest %.3f (digest %.3f), "
+                     "wait + copy + sync %.3f, total %.3f ms\n", pass_counter, t_image, t_scene - t_image,
+                     uploaded ? " (uploaded)" : "", t_launch - t_scene, t_digest, ms() - t_launch, ms());
     if (rc != PT_OK) report("path_tracer_kernel");
 }
 

@@ -629,6 +629,36 @@ def test_reference_abi_alternates_with_cpu_twin_on_managed_buffers(require_gpu):
         hip.hipFree(pimg8)
 
 
+def test_reference_abi_pass_cache_follows_camera_and_passes(require_gpu):
+    """The reference ABI renders passes ahead in batched launches and serves later calls from them
+    (pt_runtime.cpp abi_render_pass): every call must still equal the oracle's pass chain, when the camera
+    moves (the cache is keyed by the camera bytes), when the pass counter restarts, and past the end of a
+    batch (passes 1..10 cross the two 4-pass slots into a new batch)."""
+    sc = pt.cornell_scene(pt.torus_knot(40, 12), cube_length=16)
+    cfg = pt.configuration(max_tracer_depth=5)
+    cams = [pt.camera(48, 32, **BENCH_CAM), pt.camera(48, 32, yaw=0.3, **BENCH_CAM)]
+    n = 48 * 32
+    img = (pt._abi.Float3 * n)()
+    img8 = (pt._abi.UChar3 * n)()
+    scratch = [C.c_void_p() for _ in range(5)]
+    lib = pt.lib()
+    lib.path_tracer_kernel_memory_allocate(*[C.byref(s) for s in scratch], n)
+    v = sc.view
+    try:
+        for cam_i, passes in ((0, 3), (1, 2), (0, 10), (0, 1), (1, 6)):
+            cam = cams[cam_i]
+            want = np.zeros((n, 3), np.float32)
+            want8 = np.zeros((n, 3), np.uint8)
+            for p in range(1, passes + 1):
+                lib.path_tracer_kernel(v.mesh_num, v.bvh_nodes, v.triangles, v.sphere_num, v.spheres, n, img, img8, p,
+                                       C.byref(cam), v.sky_cube_map, *scratch, v.mesh_textures, C.byref(cfg))
+                oracle.render(v, cam, cfg, p, 1, image=want, image256=want8)
+                assert_bitwise(np.frombuffer(img, np.float32).reshape(-1, 3), want, f"camera {cam_i} pass {p} float")
+                assert_bitwise(np.frombuffer(img8, np.uint8).reshape(-1, 3), want8, f"camera {cam_i} pass {p} 8-bit")
+    finally:
+        lib.path_tracer_kernel_memory_free(*scratch)
+
+
 def test_reference_abi_sees_in_place_edits(require_gpu):
     """The reference ABI keeps the resident scene when a pass-1 call re-sends identical content, and must
     re-read it after an in-place edit (the reference's editor writes materials and spheres into the same

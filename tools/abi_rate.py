@@ -4,8 +4,8 @@ of the 1920x1080 metric frame through `path_tracer_kernel`, one call per pass as
 Core/path_tracer.cpp:40-67 makes them, on image buffers allocated as the reference allocates them
 (--image managed: hipMallocManaged, Core/image.cpp:15-27) or as pageable host arrays (--image host).
 Each call ends with the running sum and the 8-bit image in the caller's buffers. The scene is the
-bench scene; the first frame (scene translation and upload) is excluded; every frame's pass 1 re-checks
-the scene (the reference resets pass_counter after a camera move).
+bench scene; the first frame (scene translation and upload) is excluded; the camera moves between
+frames and every frame's pass 1 re-checks the scene (the reference resets pass_counter after a move).
 
     python tools/abi_rate.py [--frames F] [--image managed|host]
 """
@@ -25,7 +25,7 @@ import pathtracerwithcuda_amd as pt  # noqa: E402
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=4)
     ap.add_argument("--image", choices=["managed", "host"], default="managed")
     args = ap.parse_args()
     wl = bench.Workload("metric")
@@ -49,19 +49,22 @@ def main() -> None:
     lib.path_tracer_kernel_memory_allocate(*[C.byref(s) for s in scratch], n)
 
     per_pass = [0.0] * (wl.spp + 1)
+    # the camera moves between frames, as it does when the reference caller resets pass_counter
+    # (Core/path_tracer.cpp:101-107): every frame's pass 1 is a new render, never a repeat
+    cams = [cam, pt.camera(wl.width, wl.height, yaw=1e-3, **bench.CAMERA)]
 
-    def frame() -> None:
+    def frame(c) -> None:
         for p in range(1, wl.spp + 1):
             t = time.perf_counter()
             lib.path_tracer_kernel(v.mesh_num, v.bvh_nodes, v.triangles, v.sphere_num, v.spheres, n, img, img8, p,
-                                   C.byref(cam), v.sky_cube_map, *scratch, v.mesh_textures, C.byref(cfg))
+                                   C.byref(c), v.sky_cube_map, *scratch, v.mesh_textures, C.byref(cfg))
             per_pass[p] += time.perf_counter() - t
 
-    frame()  # scene translation + upload on the first pass
+    frame(cams[1])  # scene translation + upload on the first pass
     per_pass[:] = [0.0] * (wl.spp + 1)
     t0 = time.perf_counter()
-    for _ in range(args.frames):
-        frame()
+    for f in range(args.frames):
+        frame(cams[f % 2])
     dt = (time.perf_counter() - t0) / args.frames
     lib.path_tracer_kernel_memory_free(*scratch)
     if hip is not None:
