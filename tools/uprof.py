@@ -52,7 +52,7 @@ d["drained_lanes_per_walk_step"] = round(d["drained_walking_lanes"] / max(d["dra
 d["next_segment_frac_of_shade"] = round(d["cyc_next_segment"] / max(d["cyc_shade"], 1), 3)
 # timeline (stats[32..41], real-time clock at 100 MHz): waves' start, first drained refill, end
 M = (1 << 64) - 1
-tl = v[32:42]
+tl = v[32:44]
 if tl[8]:
     t0 = M ^ tl[0]
     us = lambda t: round((t - t0) / 100.0, 1)  # noqa: E731
@@ -65,4 +65,7 @@ if tl[8]:
     d["tl_wave_tail_avg_us"] = round(tl[6] / tl[8] / 100.0, 1)
     d["tl_wave_life_avg_us"] = round(tl[7] / tl[8] / 100.0, 1)
     d["tl_segments_after_drain_frac"] = round(tl[9] / max(d["segments"], 1), 3)
+    d["gen_batches"] = tl[10]
+    d["lanes_per_gen_batch"] = round(d["refilled"] / max(tl[10], 1), 2)
+    d["live_lanes_per_round"] = round(tl[11] / max(d["rounds"], 1), 2)
 print(json.dumps(d))
