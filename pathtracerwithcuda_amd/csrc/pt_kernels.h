@@ -18,11 +18,10 @@
 namespace pt {
 
 // Which pass kernel a render launches (pt_runtime.cpp pass_choice): leaf size 1, instrumented, the
-// scene's reachable features (pt_path.h PT_FEAT_*), quantised nodes.
+// scene's reachable features (pt_path.h PT_FEAT_*).
 struct PassChoice {
     bool leaf1, stats;
     int feat;
-    bool qn;  // the scene has quantised nodes: pass_kernel_u walks them (QN instance)
 };
 hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int first_pass, int batch_log2,
                        int write_u8, int grid, int lds_bytes, hipStream_t stream);

@@ -318,7 +318,7 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
 // batches, lanes in triangle batches, lanes refilled, then cycles and the drained/ready/idle counts,
 // and the launch timeline in stats[32..41].
 // FEAT: the scene features shade_hit can reach (pt_path.h PT_FEAT_*).
-template <int MINW, bool PROF, int FEAT, bool QN = false>
+template <int MINW, bool PROF, int FEAT>
 __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
                                                                 int walk_steps, int tri_min, int walk_min) {
@@ -367,7 +367,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     MeshWalk w;
     int mesh = 0;
     int ptri = -1;  // leaf triangle awaiting its test (LANE_TRI)
-    bool qlane = false;  // QN: this segment's 1/d is finite, so it walks the quantised nodes (pt_path.h)
     unsigned int unit = 0;
     int32_t pseed = 0;
     int depth = 0;
@@ -444,7 +443,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         if (mode == LANE_NEW) {
             if (roots) mode = begin_segment_roots(sc, lds_mesh, lds_root, ps, inv, h, w, mesh);
             else mode = begin_segment(sc, ps, inv, h, w, mesh);
-            if (QN) qlane = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
         }
         if (!__any(mode != LANE_DONE)) break;
         if (PROF) { const unsigned long long t = __builtin_readcyclecounter(); prof[8] += t - tc; tc = t; }
@@ -482,9 +480,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         }
 
         const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
-        const __amdgpu_buffer_rsrc_t rt = QN ? make_rsrc(sc.qtri, sc.tri_count * 64) : make_rsrc(sc.tri_geom, sc.tri_count * 48);
-        const __amdgpu_buffer_rsrc_t rq = QN ? make_rsrc(sc.qnodes, sc.node_count * 16) : rn;
-        const float4 qfb = sc.qframe[0], qfs = sc.qframe[1];
+        const __amdgpu_buffer_rsrc_t rt = make_rsrc(sc.tri_geom, sc.tri_count * 48);
         // closest_hit's merge of a finished mesh walk (:443-454), then the next mesh or READY
         auto mesh_done = [&]() {
             if (w.tri >= 0 && w.t < h.t) {
@@ -502,7 +498,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         };
         // the parked triangle's geometry, loaded at the park; scoped to the walk loop, which no lane leaves
         // parked (the last step flushes the batch), so it is not live across shading
-        float4 pta = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ptb = pta, ptc = pta, ptd = pta;
+        float4 pta = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ptb = pta, ptc = pta;
         for (int k = 0; k < walk_steps; k++) {
             if (k > 0 && !__any(mode == LANE_WALK || mode == LANE_TRI)) break;
             if (PROF) {
@@ -525,18 +521,10 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     bool l2 = walk_box_chain<2>(rn, o2, i2, w2, t2);
                     opaque(w2); opaque(l2); opaque(t2);
                 }
-                bool leaf;
-                if (QN && qlane) leaf = walk_box_chain_q(rq, qfb, qfs, ps.o, inv, w, ptri);
-                else leaf = walk_box_chain<2>(rn, ps.o, inv, w, ptri);
-                if (leaf) {
+                if (walk_box_chain<2>(rn, ps.o, inv, w, ptri)) {
                     // a leaf whose box passes: the lane parks, its triangle's loads in flight while the batch fills
                     mode = LANE_TRI;
-                    if (QN) {  // the 64-B record: the triangle and the leaf's exact box
-                        pta = bload(rt, ptri * 64); ptb = bload(rt, ptri * 64 + 16); ptc = bload(rt, ptri * 64 + 32);
-                        ptd = bload(rt, ptri * 64 + 48);
-                    } else {
-                        pta = bload(rt, ptri * 48); ptb = bload(rt, ptri * 48 + 16); ptc = bload(rt, ptri * 48 + 32);
-                    }
+                    pta = bload(rt, ptri * 48); ptb = bload(rt, ptri * 48 + 16); ptc = bload(rt, ptri * 48 + 32);
                 }
             }
             // leaf triangles are tested in batches of at least tri_min lanes (or when no lane can walk on,
@@ -552,8 +540,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                         walk_tri_geom(a2, b2, c2, o2, d2, w2, t2);
                         opaque(w2);
                     }
-                    if (QN) walk_tri_q(pta, ptb, ptc, ptd, ps.o, ps.d, inv, w, ptri);
-                    else walk_tri_geom(pta, ptb, ptc, ps.o, ps.d, w, ptri);
+                    walk_tri_geom(pta, ptb, ptc, ps.o, ps.d, w, ptri);
                     mode = LANE_WALK;
                 }
             }
@@ -858,26 +845,13 @@ using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int,
 // pass_kernel_u specialised on the scene's features (pt_path.h PT_FEAT_*): feat is what the scene can reach;
 // PT_FEAT_SPECIALISE=0 keeps the all-features kernel. `feat_used` receives the instance's features, so the
 // kernel description names the kernel that runs. PT_UPROF=1: the profiling instance (6 waves, all features).
-static PassFnU pass_fn_u(int minw, int feat, bool qn, int* feat_used, int* minw_used) {
+static PassFnU pass_fn_u(int minw, int feat, int* feat_used, int* minw_used) {
     static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
     static const int prof = env_int("PT_UPROF", 0, 0, 1);
     if (!spec) feat = PT_FEAT_ALL;
-    if (prof) {
-        *feat_used = PT_FEAT_ALL; *minw_used = 6;
-        return qn ? pass_kernel_u<6, true, PT_FEAT_ALL, true> : pass_kernel_u<6, true, PT_FEAT_ALL>;
-    }
+    if (prof) { *feat_used = PT_FEAT_ALL; *minw_used = 6; return pass_kernel_u<6, true, PT_FEAT_ALL>; }
     *feat_used = feat;
     *minw_used = minw;
-    if (qn) {  // quantised-node instances: 6 and 7 waves
-        *minw_used = minw == 7 ? 7 : 6;
-#define PT_UQ_CASE(W, F) case W * 4 + F: return pass_kernel_u<W, false, F, true>;
-        switch ((minw == 7 ? 7 : 6) * 4 + feat) {
-            PT_UQ_CASE(6, 0) PT_UQ_CASE(6, 1) PT_UQ_CASE(6, 2) PT_UQ_CASE(6, 3)
-            PT_UQ_CASE(7, 0) PT_UQ_CASE(7, 1) PT_UQ_CASE(7, 2) PT_UQ_CASE(7, 3)
-            default: break;
-        }
-#undef PT_UQ_CASE
-    }
 #define PT_U_CASE(W, F) case W * 4 + F: return pass_kernel_u<W, false, F>;
     switch (minw * 4 + feat) {
         PT_U_CASE(5, 0) PT_U_CASE(5, 1) PT_U_CASE(5, 2) PT_U_CASE(5, 3)
@@ -910,7 +884,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
         static const int tri_min = env_int("PT_TRI_MIN", 6, 1, 64);
         static const int walk_min = env_int("PT_WALK_MIN", 8, 0, 64);
         int fu, wu;
-        const PassFnU fn = pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, pc.qn, &fu, &wu);
+        const PassFnU fn = pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, &fu, &wu);
         const LaunchParams* a0 = params_dev;
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
             a8 = walk_min;
@@ -951,9 +925,9 @@ std::string pass_kernel_desc(const PassChoice& pc, int lds_bytes) {
     char buf[160];
     if (use_unified(pc.leaf1, pc.stats, lds_bytes)) {
         int fu, wu;
-        (void)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, pc.qn, &fu, &wu);
+        (void)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, &fu, &wu);
         static const int prof = env_int("PT_UPROF", 0, 0, 1);
-        std::snprintf(buf, sizeof(buf), "pass_kernel_u<MINW=%d,FEAT=%d%s%s>", wu, fu, pc.qn ? ",QN" : "", prof ? ",PROF" : "");
+        std::snprintf(buf, sizeof(buf), "pass_kernel_u<MINW=%d,FEAT=%d%s>", wu, fu, prof ? ",PROF" : "");
     } else {
         std::snprintf(buf, sizeof(buf), "pass_kernel<LEAF1=%d,STATS=%d,MINW=%d>", pc.leaf1 ? 1 : 0, pc.stats ? 1 : 0,
                       pass_min_waves(false, pc.feat));
@@ -968,7 +942,7 @@ int pass_grid_size(const PassChoice& pc, int lds_bytes) {
     if (cus <= 0) cus = 256;
     const bool u = use_unified(pc.leaf1, pc.stats, lds_bytes);
     int fu, wu;
-    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, pc.qn, &fu, &wu)
+    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, &fu, &wu)
                        : (const void*)pass_fn(pc.leaf1, pc.stats, pass_min_waves(false, pc.feat));
     const size_t lds = u ? (size_t)lds_bytes : 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, u ? PT_UBLOCK : PT_BLOCK, lds) != hipSuccess || blocks <= 0)

@@ -423,62 +423,6 @@ __device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, 
     return chain_test<CHAIN>(r, o, inv, w, tri);
 }
 
-// ---- the same step on quantised nodes (DevScene::qnodes; scenes whose tree misses the L2) -------------
-// Two 16-B records instead of two 32-B ones. Each box is rounded outward in the scene-wide frame, so it
-// contains the exact box: for a lane whose 1/d is finite, the slab arithmetic is monotone in the planes,
-// and a quantised test passes wherever the exact one does. The walk therefore visits every node the
-// reference visits (plus some), in preorder; a leaf it parks on counts only if the leaf's EXACT test
-// passes too (walk_tri_q, in the triangle batch, under the current min_t). In a scene with nested boxes
-// (DevScene::nested) an exact leaf pass implies every exact ancestor pass under the larger min_t it was
-// visited with (the argument of pt_kernels.hip's leaf-by-leaf experiment, and of round 2's wide walk):
-// the leaves tested, their order and min_t are the reference's. Lanes whose 1/d is not finite walk the
-// exact nodes (walk_box_chain<2>).
-__device__ __forceinline__ float dequant(float origin, float step, unsigned int q) { return origin + (float)q * step; }
-__device__ __forceinline__ void qbox(const u32x4 q, const float4 fb, const float4 fs, float4& lo, float4& hi) {
-    lo.x = dequant(fb.x, fs.x, q.x & 0xffffu);
-    lo.y = dequant(fb.y, fs.y, q.x >> 16);
-    lo.z = dequant(fb.z, fs.z, q.y & 0xffffu);
-    hi.x = dequant(fb.x, fs.x, q.y >> 16);
-    hi.y = dequant(fb.y, fs.y, q.z & 0xffffu);
-    hi.z = dequant(fb.z, fs.z, q.z >> 16);
-}
-__device__ __forceinline__ bool walk_box_chain_q(const __amdgpu_buffer_rsrc_t rq, const float4 fb, const float4 fs, v3 o,
-                                                 v3 inv, MeshWalk& w, int& tri) {
-    const u32x4 q0 = __builtin_amdgcn_raw_buffer_load_b128(rq, w.pos * 16, 0, 0);
-    const u32x4 q1 = __builtin_amdgcn_raw_buffer_load_b128(rq, w.pos * 16 + 16, 0, 0);
-    asm volatile("" ::"v"(q1.w));  // both records issued together (chain_load)
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const u32x4 q = i ? q1 : q0;
-        float4 lo, hi;
-        qbox(q, fb, fs, lo, hi);
-        const int link = (int)q.w;
-        float entry;
-        if (box_hit(lo, hi, o, inv, &entry) && entry <= w.t) {
-            if (link < 0) {
-                tri = link & 0x7fffffff;
-                return true;
-            }
-            w.pos++;
-        } else {
-            w.pos = link < 0 ? w.pos + 1 : link;
-            return false;
-        }
-    }
-    return false;
-}
-// The triangle batch of a QN walk: the 64-B record {v0, lo.x}, {e1, lo.y}, {e2, lo.z}, {hi.xyz, -} (qtri)
-// carries the leaf's exact box; the triangle counts only where the exact leaf test passes.
-__device__ __forceinline__ void walk_tri_q(float4 a, float4 b, float4 c, float4 h, v3 o, v3 d, v3 inv, MeshWalk& w,
-                                           int tri) {
-    float e, t, t1, t2;
-    if (box_hit(make_float4(a.w, b.w, c.w, 0.0f), h, o, inv, &e) && e <= w.t &&
-        triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t) {
-        w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
-    }
-    w.pos++;
-}
-
 // The leaf's triangle test (triangle.h:27-62, accepted when t > 0 && t < min_t, :128) with its records
 // already loaded, then the walk moves past the leaf.
 __device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri) {

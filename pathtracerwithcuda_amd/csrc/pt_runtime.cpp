@@ -457,7 +457,7 @@ struct pt_context {
     unsigned int* band_cost = nullptr;
     int band_cost_n = 0;
     bool band_cost_on = false;
-    int grid[2][2][2][4] = {};
+    int grid[2][2][4] = {};
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
     size_t ev_used = 0;
@@ -569,113 +569,9 @@ int nodes_nested(const std::vector<float4>& nodes, const std::vector<int2>& rang
     return 1;
 }
 
-// ---- quantised nodes for trees that miss the L2 (pass_kernel_u QN, pt_path.h walk_box_chain_q) --------
-// 16-bit fixed-point node boxes in one scene-wide frame: the dequantised plane is origin + (float)q * step
-// (two IEEE operations, no contraction, the same on the device), q chosen so that the plane lies outside
-// or on the exact one. A record is 16 B: lo.xyz, hi.xyz as u16, then the link (internal: next node; leaf:
-// 0x80000000 | triangle). With them the leaves' exact boxes travel with their triangles (qtri, 64 B:
-// {v0, lo.x}, {e1, lo.y}, {e2, lo.z}, {hi.xyz, -}) for the exact leaf test in the triangle batch.
-float dequant(float origin, float step, unsigned q) { return origin + (float)q * step; }
-
-unsigned quant_down(float origin, float step, float v) {
-    if (!(step > 0.0f)) return 0;
-    double f = std::floor(((double)v - (double)origin) / (double)step);
-    long long q = f < 0 ? 0 : (f > 65535 ? 65535 : (long long)f);
-    while (q > 0 && dequant(origin, step, (unsigned)q) > v) q--;
-    while (q < 65535 && dequant(origin, step, (unsigned)q + 1) <= v) q++;
-    return (unsigned)q;
-}
-
-unsigned quant_up(float origin, float step, float v) {
-    if (!(step > 0.0f)) return 0;
-    double f = std::ceil(((double)v - (double)origin) / (double)step);
-    long long q = f < 0 ? 0 : (f > 65535 ? 65535 : (long long)f);
-    while (q < 65535 && dequant(origin, step, (unsigned)q) < v) q++;
-    while (q > 0 && dequant(origin, step, (unsigned)q - 1) >= v) q--;
-    return (unsigned)q;
-}
-
-// Whether a scene gets quantised nodes: PT_QNODES=1 always, 0 never (default, until measured), -1: when the
-// node array exceeds PT_QNODES_MB (default 16 MB, four times an XCD's L2) — the bench scene's 4.5 MB tree
-// stays exact.
-bool want_qnodes(size_t node_bytes) {
-    static const int mode = env_int("PT_QNODES", 0, -1, 1);
-    static const int mb = env_int("PT_QNODES_MB", 16, 0, 1 << 20);
-    if (mode >= 0) return mode == 1;
-    return node_bytes > (size_t)mb << 20;
-}
-
-// Fills q / qtri / frame from st (leaf size 1, nested boxes). False when a node is not representable
-// (non-finite box, a leaf whose skip index is not pos + 1, a plane outside the frame): no QN walk then.
-bool quantise_nodes(const SceneStage& st, std::vector<uint4>& q, std::vector<float4>& qtri, float4 frame[2]) {
-    q.clear();
-    qtri.clear();
-    if (st.leaf_size != 1 || st.nodes.empty()) return false;
-    const size_t N = st.nodes.size() / 2;
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (size_t i = 0; i < N; i++) {
-        const float4& a = st.nodes[2 * i];
-        const float4& b = st.nodes[2 * i + 1];
-        const float l[3] = {a.x, a.y, a.z}, h[3] = {b.x, b.y, b.z};
-        for (int k = 0; k < 3; k++) {
-            if (!std::isfinite(l[k]) || !std::isfinite(h[k])) return false;
-            lo[k] = std::min(lo[k], l[k]);
-            hi[k] = std::max(hi[k], h[k]);
-        }
-    }
-    float step[3] = {0.0f, 0.0f, 0.0f};
-    for (int k = 0; k < 3; k++) {
-        if (hi[k] <= lo[k]) continue;
-        step[k] = (float)(((double)hi[k] - (double)lo[k]) / 65534.0);
-        if (!(step[k] > 0.0f)) step[k] = std::numeric_limits<float>::denorm_min();
-        while (dequant(lo[k], step[k], 65535u) < hi[k]) step[k] = std::nextafter(step[k], INFINITY);
-    }
-    frame[0] = mkf4(lo[0], lo[1], lo[2], 0.0f);
-    frame[1] = mkf4(step[0], step[1], step[2], 0.0f);
-    q.resize(N);
-    const size_t T = st.tri_geom.size() / 3;
-    qtri.assign(T * 4, mkf4(0.0f, 0.0f, 0.0f, 0.0f));
-    for (size_t t = 0; t < T; t++)
-        for (int k = 0; k < 3; k++) qtri[4 * t + k] = st.tri_geom[3 * t + k];
-    for (const int2& r : st.mesh_range) {
-        for (int i = r.x; i < r.y; i++) {
-            const float4& a = st.nodes[2 * i];
-            const float4& b = st.nodes[2 * i + 1];
-            const float l[3] = {a.x, a.y, a.z}, h[3] = {b.x, b.y, b.z};
-            unsigned ql[3], qh[3];
-            for (int k = 0; k < 3; k++) {
-                ql[k] = quant_down(lo[k], step[k], l[k]);
-                qh[k] = quant_up(lo[k], step[k], h[k]);
-                if (dequant(lo[k], step[k], ql[k]) > l[k] || dequant(lo[k], step[k], qh[k]) < h[k]) return false;
-            }
-            const int next = f2i_host(a.w), slot = f2i_host(b.w);
-            uint4 n;
-            n.x = ql[0] | (ql[1] << 16);
-            n.y = ql[2] | (qh[0] << 16);
-            n.z = qh[1] | (qh[2] << 16);
-            if (slot >= 0) {
-                if (next != i + 1 || (size_t)slot >= T) return false;
-                n.w = 0x80000000u | (unsigned)slot;
-                float4* r4 = &qtri[4 * (size_t)slot];  // the leaf's exact box with its triangle
-                r4[0].w = a.x; r4[1].w = a.y; r4[2].w = a.z;
-                r4[3] = mkf4(b.x, b.y, b.z, 0.0f);
-            } else {
-                n.w = (unsigned)next;
-            }
-            q[i] = n;
-        }
-    }
-    return true;
-}
-
 int upload_stage(pt_context* ctx, const SceneStage& st) {
     ctx->spec_valid = false;
     const int nested = nodes_nested(st.nodes, st.mesh_range);
-    std::vector<uint4> qn;
-    std::vector<float4> qtri;
-    float4 qframe[2] = {mkf4(0, 0, 0, 0), mkf4(0, 0, 0, 0)};
-    const bool qok = nested && want_qnodes(st.nodes.size() * sizeof(float4)) && quantise_nodes(st, qn, qtri, qframe);
-    if (!qok) { qn.clear(); qtri.clear(); }
     struct Piece { const void* src; size_t bytes; size_t off; };
     std::vector<Piece> pieces;
     size_t total = 0;
@@ -695,8 +591,6 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
     size_t i_tex = add(st.tex_desc.data(), st.tex_desc.size() * sizeof(int4));
     size_t i_pool = add(st.tex_pool.data(), st.tex_pool.size());
     size_t i_cube = add(st.cube.data(), st.cube.size());
-    size_t i_qn = add(qn.data(), qn.size() * sizeof(uint4));
-    size_t i_qtri = add(qtri.data(), qtri.size() * sizeof(float4));
     free_scene(ctx);
     if (total == 0) total = 256;
     PT_HIP(hipMalloc(&ctx->scene_mem, total));
@@ -732,10 +626,6 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
             break;
         }
     s.nested = nested;
-    s.qnodes = qok ? (const uint4*)(base + pieces[i_qn].off) : nullptr;
-    s.qtri = qok ? (const float4*)(base + pieces[i_qtri].off) : nullptr;
-    s.qframe[0] = qframe[0];
-    s.qframe[1] = qframe[1];
     ctx->node_num = (int)(st.nodes.size() / 2);
     ctx->mesh_range = st.mesh_range;
     ctx->tri_num = (int)(st.tri_geom.size() / 3);
@@ -840,13 +730,12 @@ PassChoice pass_choice(const pt_context* ctx, int feat) {
     pc.leaf1 = ctx->scene.leaf_size == 1;
     pc.stats = ctx->instrumented;
     pc.feat = feat;
-    pc.qn = ctx->scene.qnodes != nullptr;
     return pc;
 }
 
 int pass_grid(pt_context* ctx, int feat) {
     const PassChoice pc = pass_choice(ctx, feat);
-    int& g = ctx->grid[pc.leaf1 ? 1 : 0][pc.stats ? 1 : 0][pc.qn ? 1 : 0][feat & 3];
+    int& g = ctx->grid[pc.leaf1 ? 1 : 0][pc.stats ? 1 : 0][feat & 3];
     if (g == 0) {
         g = pass_grid_size(pc, pass_lds_bytes(ctx));
         // PT_GRID_PCT: experiment knob, a percentage of the occupancy-sized grid
@@ -1408,8 +1297,6 @@ extern "C" int pt_mesh_set_transform(pt_context* ctx, int mesh, pt_float3 positi
     ctx->resident_valid = false;  // the resident scene no longer equals its last upload
     ctx->raw_valid = false;
     ctx->spec_valid = false;
-    ctx->scene.qnodes = nullptr;  // the quantised records hold the pre-refit boxes: walk the exact nodes
-    ctx->scene.qtri = nullptr;
     std::memset(ctx->grid, 0, sizeof(ctx->grid));
     return PT_OK;
 }

@@ -74,12 +74,6 @@ struct DevScene {
     int first_mesh;    // first mesh with a non-empty node range (mesh_num if none) and that range:
     int2 first_range;  //   where every trace step's mesh walk starts
     int nested;        // 1: every node's box contains its children's boxes
-    // quantised nodes (large trees only; pt_runtime.cpp quantise_nodes): 16 B per node, same preorder
-    // index as `nodes`, in the scene-wide frame qframe = {origin}, {step}; qtri = 64-B triangle records with
-    // the leaf's exact box; both null when the scene walks the exact nodes
-    const uint4* qnodes;
-    const float4* qtri;
-    float4 qframe[2];
 };
 
 // The subset of Core/configuration.h:9-34 that the kernel reads.
