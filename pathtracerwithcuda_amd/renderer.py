@@ -42,6 +42,26 @@ def camera(width: int, height: int, fov: float = 45.0, yaw: float = 0.0, pitch: 
     return rc
 
 
+def deal_bands(ranked: list[int], n: int, regions: int) -> list[int]:
+    """Band order for `n` local bands (positions n - len(ranked) .. n - 1 beyond the ranked ones keep
+    their band: the partial last band) whose units a launch cuts into `regions` equal contiguous
+    regions: position p belongs to the region holding its midpoint, and the ranked bands go out
+    round-robin over the regions, each filling its positions front to back."""
+    slots: list[list[int]] = [[] for _ in range(regions)]
+    for p in range(len(ranked)):
+        slots[min(regions - 1, (2 * p + 1) * regions // (2 * n))].append(p)
+    order = list(range(n))
+    fill = [0] * regions
+    r = 0
+    for b in ranked:
+        while fill[r] == len(slots[r]):
+            r = (r + 1) % regions
+        order[slots[r][fill[r]]] = b
+        fill[r] += 1
+        r = (r + 1) % regions
+    return order
+
+
 class Renderer:
     """One device context: resident scene, resident accumulation image, one HIP stream."""
 
@@ -108,9 +128,14 @@ class Renderer:
         check(self._lib.pt_band_cost(self._ctx, a, n), "pt_band_cost")
         return [int(x) for x in a]
 
-    def order_bands_by_cost(self, cam: RenderCamera, config: Configuration, passes: int) -> list[int]:
+    def order_bands_by_cost(self, cam: RenderCamera, config: Configuration, passes: int,
+                            regions: int = 1) -> list[int]:
         """Render one (untimed) frame measuring each band's ray segments, then hand the bands out most
-        expensive first (a partial last band stays last). Returns the order."""
+        expensive first (a partial last band stays last). Returns the order.
+
+        regions > 1: the launch cuts its units into that many contiguous regions (PT_SHARDS = 8, one
+        per XCD, pt_work.h), each handed out front to back; the ranked bands are then dealt round-robin
+        over the regions' band slots, so that every region starts on its most expensive bands."""
         self.set_band_order(None)
         self.measure_band_cost(True)
         self.render(cam, config, 1, passes, write_u8=0)
@@ -118,7 +143,8 @@ class Renderer:
         self.measure_band_cost(False)
         n, partial = self.band_count()
         full = n - 1 if partial else n
-        order = sorted(range(full), key=lambda b: (-cost[b], b)) + ([n - 1] if partial else [])
+        ranked = sorted(range(full), key=lambda b: (-cost[b], b))
+        order = deal_bands(ranked, n, regions) if regions > 1 else ranked + ([n - 1] if partial else [])
         self.set_band_order(order)
         return order
 

@@ -114,6 +114,30 @@ def test_owned_pixels_partition_the_frame():
             assert all((y // BAND) % world == k for y in rows)
 
 
+@pytest.mark.parametrize("n,partial", [(17, True), (135, True), (16, False), (5, False), (9, True)])
+def test_deal_bands_gives_every_region_its_costliest_bands_first(n, partial):
+    """renderer.deal_bands: a permutation of the local bands that keeps a partial last band last; the
+    launch's 8 regions (band positions by midpoint) each receive ranked bands in rank order, and the
+    first band of every non-empty region comes from the top of the ranking."""
+    from pathtracerwithcuda_amd.renderer import deal_bands
+    full = n - 1 if partial else n
+    rng = np.random.default_rng(n)
+    ranked = [int(b) for b in rng.permutation(full)]
+    order = deal_bands(ranked, n, 8)
+    assert sorted(order) == list(range(n))
+    if partial:
+        assert order[-1] == n - 1
+    rank_of = {b: i for i, b in enumerate(ranked)}
+    region = [min(7, (2 * p + 1) * 8 // (2 * n)) for p in range(full)]
+    firsts = []
+    for r in range(8):
+        ranks = [rank_of[order[p]] for p in range(full) if region[p] == r]
+        assert ranks == sorted(ranks)
+        if ranks:
+            firsts.append(ranks[0])
+    assert sorted(firsts) == list(range(len(firsts)))
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world,collective,inflight", [(2, "gather", 1), (2, "reduce", 1), (3, "gather", 1),
                                                        (2, "gather", 2), (2, "reduce", 3)])

@@ -27,6 +27,8 @@ def main() -> None:
     ap.add_argument("--ranks-max", type=int, default=8, help="time at most this many ranks per N")
     ap.add_argument("--share", type=int, default=100, help="pt_set_grid_share: percent of the grid per launch")
     ap.add_argument("--order", action="store_true", help="hand out bands most expensive first (pt_set_band_order)")
+    ap.add_argument("--deal", type=int, default=1, help="with --order: deal the ranked bands over this many regions (8 = PT_SHARDS)")
+    ap.add_argument("--band-rows", type=int, default=0, help="rows per band (default bench.BAND_ROWS)")
     args = ap.parse_args()
     wl = bench.Workload("metric")
     rs = []
@@ -43,9 +45,9 @@ def main() -> None:
         per_rank, kern = [], []
         for k in range(min(n, args.ranks_max)):
             for q in rs:
-                q.set_tiling(bench.BAND_ROWS, n, k)
+                q.set_tiling(args.band_rows or bench.BAND_ROWS, n, k)
                 if args.order:
-                    q.order_bands_by_cost(wl.cam, wl.cfg, wl.spp)
+                    q.order_bands_by_cost(wl.cam, wl.cfg, wl.spp, regions=args.deal)
                 q.render(wl.cam, wl.cfg, 1, wl.spp, write_u8=0)  # warm
                 q.synchronize()
                 q.stats_reset()
