@@ -355,10 +355,16 @@ def main() -> int:
         bytes_per_launch = extend_bytes(counts, scene.view.sphere_num) / world / launches_per_frame
         kernel_name = "extend_kernel<LEAF1=true,STATS=false>"
     workload = wl.key
-    prof = load_profile(workload + ("" if schedule == "persistent" else "/wavefront"))
-    # the profiled launch is the whole 1-GPU frame; a rank of N runs 1/N of it
-    traffic = float(prof["hbm_bytes_per_launch"]) / world if prof.get("hbm_bytes_per_launch") else None
-    valu_insts = float(prof["valu_insts_per_launch"]) / world if prof.get("valu_insts_per_launch") else None
+    key = workload + ("" if schedule == "persistent" else "/wavefront")
+    # N > 1: rank 0's share profiled on its own (tools/gpu_share_pmc.sh, "<key>/tiled<N>"); otherwise the
+    # whole 1-GPU frame's profile, of which a rank of N runs 1/N
+    prof = load_profile(f"{key}/tiled{world}") if world > 1 else {}
+    per_rank = bool(prof)
+    if not per_rank:
+        prof = load_profile(key)
+    scale = 1.0 if per_rank or world == 1 else 1.0 / world
+    traffic = float(prof["hbm_bytes_per_launch"]) * scale if prof.get("hbm_bytes_per_launch") else None
+    valu_insts = float(prof["valu_insts_per_launch"]) * scale if prof.get("valu_insts_per_launch") else None
     # The resource that binds this kernel is VALU issue behind a dependent-load chain, not HBM
     # (DESIGN.md §4): a wave64 VALU instruction issues over 2 cycles of its SIMD-32
     # (MI355X_MICROARCH.md, Wave scheduling), so the chip issues at most SIMDS x clock / 2 wave-level
@@ -371,7 +377,7 @@ def main() -> int:
     valu_timed = valu_insts * launches_per_frame / (ms_per_step / 1000.0) / 1e9 if valu_insts else None
     # Lane-weighted: a wave-instruction counts active lanes / 64 (PT_UPROF lanes per phase x the PT_DUP VALU
     # split per phase, tools/lane_weighted.py, recorded in profiles/traffic.json)
-    valu_lanes = float(prof["valu_lane_weighted_per_launch"]) / world if prof.get("valu_lane_weighted_per_launch") else None
+    valu_lanes = float(prof["valu_lane_weighted_per_launch"]) * scale if prof.get("valu_lane_weighted_per_launch") else None
     hbm = None
     if traffic is not None:
         hbm_gbs = traffic / avg_launch_s / 1e9
@@ -419,6 +425,9 @@ def main() -> int:
             "frac_lane_weighted": round(valu_lanes / avg_launch_s / 1e9 / valu_peak, 4) if valu_lanes else None,
             "valu_lane_weighted_per_launch": round(valu_lanes) if valu_lanes else None,
             "kernel": kernel_name,
+            "counters_from": ("one GPU" if world == 1 else
+                              f"rank 0's share of {world}, profiled on its own" if per_rank else
+                              f"the 1-GPU frame's profile / {world}"),
             "avg_launch_ms": round(avg_launch_s * 1000, 4),
             "avg_launch_source": "HIP events on the renderer stream, one frame in flight",
             "avg_launch_ms_frames_in_flight": round(kernel_ms / max(launches, 1), 4),

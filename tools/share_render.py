@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Renders rank 0's share of the tiled metric frame (pt_set_tiling(BAND_ROWS, N, 0)), one frame at a
+time on the whole grid, as bench.py's solo launch at N GPUs does: the process to put under
+`rocprofv3 --pmc` for the per-rank counters of the N > 1 roofline (tools/gpu_share_pmc.sh).
+
+    python tools/share_render.py --n 8 [--frames 4]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import pathtracerwithcuda_amd as pt  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, required=True)
+    ap.add_argument("--frames", type=int, default=4)
+    ap.add_argument("--workload", default="metric")
+    args = ap.parse_args()
+    wl = bench.Workload(args.workload)
+    r = pt.Renderer(0)
+    r.upload(wl.scene, wl.cfg)
+    r.setup_frame(wl.width, wl.height)
+    r.set_tiling(bench.BAND_ROWS, args.n, 0)
+    for _ in range(args.frames):
+        r.render(wl.cam, wl.cfg, 1, wl.spp, write_u8=0)
+        r.synchronize()
+    ms, n = r.kernel_time_kind(0)
+    print(f"share 0 of {args.n}: {ms / max(n, 1):.3f} ms per launch over {n} launches ({r.last_kernel()})")
+    r.close()
+
+
+if __name__ == "__main__":
+    main()
