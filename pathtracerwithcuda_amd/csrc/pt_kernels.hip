@@ -480,7 +480,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         }
 
         const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
-        const __amdgpu_buffer_rsrc_t rt = make_rsrc(sc.tri_geom, sc.tri_count * 48);
         // closest_hit's merge of a finished mesh walk (:443-454), then the next mesh or READY
         auto mesh_done = [&]() {
             if (w.tri >= 0 && w.t < h.t) {
@@ -521,11 +520,8 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     bool l2 = walk_box_chain<2>(rn, o2, i2, w2, t2);
                     opaque(w2); opaque(l2); opaque(t2);
                 }
-                if (walk_box_chain<2>(rn, ps.o, inv, w, ptri)) {
-                    // a leaf whose box passes: the lane parks, its triangle's loads in flight while the batch fills
-                    mode = LANE_TRI;
-                    pta = bload(rt, ptri * 48); ptb = bload(rt, ptri * 48 + 16); ptc = bload(rt, ptri * 48 + 32);
-                }
+                // a leaf whose box passes: the lane parks with its triangle, which came with the step's records
+                if (walk_box_inline(rn, ps.o, inv, w, ptri, pta, ptb, ptc)) mode = LANE_TRI;
             }
             // leaf triangles are tested in batches of at least tri_min lanes (or when no lane can walk on,
             // or on the round's last step, so that no lane leaves the walk loop parked): the triangle test
@@ -541,6 +537,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                         opaque(w2);
                     }
                     walk_tri_geom(pta, ptb, ptc, ps.o, ps.d, w, ptri);
+                    w.pos++;  // past the leaf's triangle record too
                     mode = LANE_WALK;
                 }
             }
@@ -871,6 +868,37 @@ static PassFnU pass_fn_u(int minw, int feat, int* feat_used, int* minw_used) {
 #define PT_LDS_TABLES (32 * 1024)
 static bool use_unified(bool leaf1, bool stats, int lds_bytes) {
     return leaf1 && !stats && unified_enabled() && lds_bytes <= PT_LDS_TABLES;
+}
+
+bool pass_uses_unified(const PassChoice& pc, int lds_bytes) { return use_unified(pc.leaf1, pc.stats, lds_bytes); }
+
+// The inline-leaf copy of the node array that pass_kernel_u walks (pt_path.h walk_box_inline): record k of
+// `nodes` goes to record np[k] of `out`; a leaf (slot >= 0, one triangle per leaf) takes two records,
+// its box with e2.z in the free skip word and then its triangle from tri_geom; an internal record keeps
+// its box with the skip index remapped through np (np[R] is the end of the last mesh).
+__global__ void inline_leaves_kernel(const float4* __restrict__ nodes, const float4* __restrict__ tri_geom,
+                                     const int* __restrict__ np, int R, float4* __restrict__ out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= R) return;
+    const float4 lo = nodes[2 * k], hi = nodes[2 * k + 1];
+    const int slot = f2i(hi.w), p = np[k];
+    if (slot >= 0) {
+        const float4 a = tri_geom[3 * slot], e1 = tri_geom[3 * slot + 1], e2 = tri_geom[3 * slot + 2];
+        out[2 * p] = make_float4(lo.x, lo.y, lo.z, e2.z);
+        out[2 * p + 1] = hi;
+        out[2 * p + 2] = make_float4(a.x, a.y, a.z, e1.x);
+        out[2 * p + 3] = make_float4(e1.y, e1.z, e2.x, e2.y);
+    } else {
+        out[2 * p] = make_float4(lo.x, lo.y, lo.z, __int_as_float(np[f2i(lo.w)]));
+        out[2 * p + 1] = hi;
+    }
+}
+
+hipError_t launch_inline_leaves(const float4* nodes, const float4* tri_geom, const int* np, int R, float4* out,
+                                hipStream_t stream) {
+    if (R <= 0) return hipSuccess;
+    hipLaunchKernelGGL(inline_leaves_kernel, dim3((R + 255) / 256), dim3(256), 0, stream, nodes, tri_geom, np, R, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int first_pass, int batch_log2,

@@ -423,6 +423,42 @@ __device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, 
     return chain_test<CHAIN>(r, o, inv, w, tri);
 }
 
+// The two-record step over the inline-leaf layout (pass_kernel_u, one triangle per leaf): a leaf is
+// two records, its box record {lo, e2.z} {hi, slot} followed by its triangle {v0, e1.x} {e1.y, e1.z,
+// e2.x, e2.y}; an internal record keeps {lo, skip} {hi, -1}. A leaf's skip is always the record after
+// its triangle, so it needs no field. A step loads 64 B at pos as before: when pos is a leaf whose box
+// passes, its triangle came with it (returned in a, e1, e2; the walk is not advanced). A leaf reached
+// as the step's second record (the left child of a passing internal record) whose box passes ends the
+// step without moving on: the next step tests it again (same inputs, same result) with its triangle.
+// The nodes tested, their order and every test's outcome are the reference's.
+__device__ __forceinline__ bool walk_box_inline(const __amdgpu_buffer_rsrc_t rn, v3 o, v3 inv, MeshWalk& w, int& tri,
+                                                float4& a, float4& e1, float4& e2) {
+    const float4 lo0 = bload(rn, w.pos * 32), hi0 = bload(rn, w.pos * 32 + 16);
+    const float4 lo1 = bload(rn, w.pos * 32 + 32), hi1 = bload(rn, w.pos * 32 + 48);
+    asm volatile("" ::"v"(lo1.w), "v"(hi1.w));  // one round trip for all four loads (chain_load)
+    float entry;
+    const int slot0 = f2i(hi0.w);
+    if (box_hit(lo0, hi0, o, inv, &entry) && entry <= w.t) {
+        if (slot0 >= 0) {
+            tri = slot0;
+            a = make_float4(lo1.x, lo1.y, lo1.z, 0.0f);
+            e1 = make_float4(lo1.w, hi1.x, hi1.y, 0.0f);
+            e2 = make_float4(hi1.z, hi1.w, lo0.w, 0.0f);
+            return true;
+        }
+        w.pos++;
+        const int slot1 = f2i(hi1.w);
+        if (box_hit(lo1, hi1, o, inv, &entry) && entry <= w.t) {
+            if (slot1 < 0) w.pos++;
+        } else {
+            w.pos = slot1 >= 0 ? w.pos + 2 : f2i(lo1.w);
+        }
+        return false;
+    }
+    w.pos = slot0 >= 0 ? w.pos + 2 : f2i(lo0.w);
+    return false;
+}
+
 // The leaf's triangle test (triangle.h:27-62, accepted when t > 0 && t < min_t, :128) with its records
 // already loaded, then the walk moves past the leaf.
 __device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri) {

@@ -506,6 +506,14 @@ struct pt_context {
     hipStream_t acc_stream = nullptr;  // the ABI's per-call accumulate and download
     hipEvent_t chunk_up[4] = {nullptr, nullptr, nullptr, nullptr};  // the running sum's upload, per chunk
     std::vector<int2> mesh_range;  // node range per mesh of the resident scene
+    // one triangle per leaf: the inline-leaf node array pass_kernel_u walks (pt_path.h walk_box_inline),
+    // the record map it is built through (np, R + 1 ints), its mesh ranges and first range
+    void* il_mem = nullptr;
+    const float4* il_nodes = nullptr;
+    const int* il_np = nullptr;
+    const int2* il_range = nullptr;
+    int il_records = 0;
+    int2 il_first{0, 0};
     // pt_mesh_attach: per mesh, device copies of its mesh-local triangles (v0..v2, n0..n2 as float4) and
     // initial node corners, and the inverse of the transform of those boxes
     struct MeshRefit {
@@ -531,6 +539,12 @@ void free_refit(pt_context* ctx) {
 
 void free_scene(pt_context* ctx) {
     free_refit(ctx);
+    if (ctx->il_mem) (void)hipFree(ctx->il_mem);
+    ctx->il_mem = nullptr;
+    ctx->il_nodes = nullptr;
+    ctx->il_np = nullptr;
+    ctx->il_range = nullptr;
+    ctx->il_records = 0;
     if (ctx->scene_mem) (void)hipFree(ctx->scene_mem);
     ctx->scene_mem = nullptr;
     ctx->scene_bytes = 0;
@@ -636,6 +650,32 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
         if (m.diffuse_texture_id != -1 || m.specular_texture_id != -1) ctx->scene_feat |= PT_FEAT_TEX;
         for (int c = 0; c < 3; c++)
             if (m.absorption[c] != 0.0f || m.reduced_scattering[c] != 0.0f) ctx->scene_feat |= PT_FEAT_MEDIUM;
+    }
+    if (st.leaf_size == 1) {
+        // record k -> np[k]: every leaf with a triangle before k adds its triangle record
+        const int R = (int)(st.nodes.size() / 2);
+        std::vector<int> np((size_t)R + 1);
+        int extra = 0;
+        for (int k = 0; k < R; k++) {
+            np[(size_t)k] = k + extra;
+            if (__builtin_bit_cast(int, st.nodes[2 * (size_t)k + 1].w) >= 0) extra++;
+        }
+        np[(size_t)R] = R + extra;
+        std::vector<int2> range(st.mesh_range.size());
+        for (size_t m = 0; m < range.size(); m++) range[m] = int2{np[(size_t)st.mesh_range[m].x], np[(size_t)st.mesh_range[m].y]};
+        const size_t b_nodes = (size_t)(R + extra) * 32, b_np = ((size_t)R + 1) * 4, b_range = range.size() * 8;
+        const size_t o_np = (b_nodes + 255) & ~(size_t)255, o_range = (o_np + b_np + 255) & ~(size_t)255;
+        PT_HIP(hipMalloc(&ctx->il_mem, o_range + b_range + 8));
+        uint8_t* ib = (uint8_t*)ctx->il_mem;
+        PT_HIP(hipMemcpyAsync(ib + o_np, np.data(), b_np, hipMemcpyHostToDevice, ctx->stream));
+        if (b_range) PT_HIP(hipMemcpyAsync(ib + o_range, range.data(), b_range, hipMemcpyHostToDevice, ctx->stream));
+        ctx->il_nodes = (const float4*)ib;
+        ctx->il_np = (const int*)(ib + o_np);
+        ctx->il_range = (const int2*)(ib + o_range);
+        ctx->il_records = R + extra;
+        ctx->il_first = s.first_mesh < (int)range.size() ? range[(size_t)s.first_mesh] : int2{0, 0};
+        PT_HIP(launch_inline_leaves(s.nodes, s.tri_geom, ctx->il_np, R, const_cast<float4*>(ctx->il_nodes), ctx->stream));
+        PT_HIP(hipStreamSynchronize(ctx->stream));
     }
     ctx->has_scene = true;
     std::memset(ctx->grid, 0, sizeof(ctx->grid));  // occupancy depends on the LDS material table
@@ -838,6 +878,10 @@ bool use_wavefront() {
 
 // The launch parameter block of a render call (without pass_rad), plus the per-material shading constants
 // for the configured air index when they are stale.
+bool wavefront_schedule(const pt_context* ctx) {
+    return ctx->schedule == PT_SCHEDULE_WAVEFRONT || (ctx->schedule < 0 && use_wavefront());
+}
+
 int prepare_launch(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config, LaunchParams& lp) {
     if (!ctx->has_scene) { set_error("no scene uploaded"); return PT_E_STATE; }
     if (!ctx->image) { set_error("no frame set up"); return PT_E_STATE; }
@@ -853,6 +897,13 @@ int prepare_launch(pt_context* ctx, const pt_render_camera* cam, const pt_config
     out.stats = ctx->stats;
     lp = LaunchParams{};
     lp.sc = ctx->scene;
+    if (ctx->il_nodes && !wavefront_schedule(ctx) &&
+        pass_uses_unified(pass_choice(ctx, render_feat(ctx, dc)), pass_lds_bytes(ctx))) {
+        lp.sc.nodes = ctx->il_nodes;  // pass_kernel_u walks the inline-leaf copy
+        lp.sc.mesh_range = ctx->il_range;
+        lp.sc.node_count = ctx->il_records;
+        lp.sc.first_range = ctx->il_first;
+    }
     lp.cfg = dc;
     lp.cam = dcam;
     lp.til = ctx->tiling;
@@ -869,10 +920,6 @@ int prepare_launch(pt_context* ctx, const pt_render_camera* cam, const pt_config
         ctx->mat_air_n_valid = true;
     }
     return PT_OK;
-}
-
-bool wavefront_schedule(const pt_context* ctx) {
-    return ctx->schedule == PT_SCHEDULE_WAVEFRONT || (ctx->schedule < 0 && use_wavefront());
 }
 
 int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config, int first_pass,
@@ -1294,6 +1341,9 @@ extern "C" int pt_mesh_set_transform(pt_context* ctx, int mesh, pt_float3 positi
     PT_HIP(launch_mesh_refit(local, m.tri_start, m.tri_count, init, ctx->mesh_range[mesh].x, m.node_count, T, Tn, C,
                              const_cast<float4*>(ctx->scene.tri_geom), const_cast<float4*>(ctx->scene.tri_shade),
                              const_cast<float4*>(ctx->scene.nodes), ctx->stream));
+    if (ctx->il_nodes)
+        PT_HIP(launch_inline_leaves(ctx->scene.nodes, ctx->scene.tri_geom, ctx->il_np, ctx->node_num,
+                                    const_cast<float4*>(ctx->il_nodes), ctx->stream));
     ctx->resident_valid = false;  // the resident scene no longer equals its last upload
     ctx->raw_valid = false;
     ctx->spec_valid = false;

@@ -11,6 +11,10 @@
 //              [mesh_range[m].x, mesh_range[m].y)  (reference: bvh_nodes[m][0].next_node_index)
 //   leaf_tris  int[L*leaf_size]  triangle ids per leaf, -1 padded (bvh.cpp:296-300)
 //              when leaf_size == 1 the slot field holds the triangle id directly
+//   nodes (inline leaves, leaf_size == 1; the array pass_kernel_u walks, built by inline_leaves_kernel
+//              from nodes + tri_geom and handed over in LaunchParams.sc): an internal node as above, a
+//              leaf two records {lb.xyz, e2.z}, {rt.xyz, triangle id}, {v0.xyz, e1.x}, {e1.yz, e2.xy}
+//              (its next index is the record after them); 32 B/internal node + 64 B/leaf
 //   tri_geom   float4[3*T]  {v0.xyz, -}, {v1-v0}, {v2-v0}                       48 B/tri
 //   tri_shade  float4[4*T]  {n0.xyz, n1.x}, {n1.yz, n2.xy}, {n2.z, uv0.xy, uv1.x},
 //                           {uv1.y, uv2.xy, material id (int bits)}             64 B/tri
@@ -141,6 +145,7 @@ struct DevOutput {
 //              cut into PT_SHARDS regions of seg_cap = ceil(units / PT_SHARDS).
 //   heads      PT_HEAD_SET uints per launch of a pass (extend d: 2d, shade d: 2d + 1), pt_work.h
 #define PT_SHARDS 8
+
 struct DevWave {
     float4* q_o[2];
     float4* q_d[2];
