@@ -642,8 +642,10 @@ __global__ __launch_bounds__(PT_BLOCK) void material_consts_kernel(DevMaterial* 
     if (i >= n) return;
     DevMaterial& m = mats[i];
     m.rough_alpha = pow_pt(m.roughness, 1.85f) * 0.238f;
-    m.tir_front = asin_pt(m.refraction_index / air_n);
-    m.tir_back = asin_pt(air_n / m.refraction_index);
+    m.ratio_front = air_n / m.refraction_index;
+    m.ratio_back = m.refraction_index / air_n;
+    m.tir_front = asin_pt(m.ratio_back);
+    m.tir_back = asin_pt(m.ratio_front);
 }
 
 hipError_t launch_material_consts(DevMaterial* mats, int n, float air_n, hipStream_t stream) {

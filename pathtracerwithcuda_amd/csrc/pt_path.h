@@ -58,11 +58,11 @@ __device__ __forceinline__ v3 reflection(v3 n, v3 in) {
     return in - 2.0f * dot(n, in) * n;
 }
 
-// path_tracer_kernel.cu:54-83
-__device__ __forceinline__ v3 refraction(v3 n, v3 in, float in_n, float out_n) {
+// path_tracer_kernel.cu:54-83; ratio = in_n / out_n (a per-material constant, DevMaterial::ratio_front /
+// ratio_back, computed by material_consts_kernel with the same division)
+__device__ __forceinline__ v3 refraction(v3 n, v3 in, float ratio) {
     v3 i = in * -1.0f;
     float ndi = dot(n, i);
-    float ratio = in_n / out_n;
     float a = ratio * ndi;
     float b = 1.0f - ratio * ratio * (1.0f - ndi * ndi);
     if (b < 0.0f) return mk3(0.0f, 0.0f, 0.0f);
@@ -256,21 +256,6 @@ __device__ __forceinline__ bool sphere_t(float4 s, v3 o, v3 d, float* t_out) {
     if (t1 < 0 && t2 < 0) return false;
     *t_out = (t1 > 0 && t2 > 0) ? fminf(t1, t2) : fmaxf(t1, t2);
     return true;
-}
-
-// 1.0f / x correctly rounded (the IEEE division of the reference and the oracle), from v_rcp_f32
-// (1 ulp) refined by one Newton step with an exact FMA residual: 3 instructions instead of the 10 of
-// the division sequence. test_rcp_exact_matches_division checks every significand in [1, 2) at several
-// exponents; outside [2^-125, 2^125] (denormal or overflowing reciprocals, 0, inf, NaN) the division
-// itself runs.
-__device__ __forceinline__ float rcp_exact(float x) {
-    const float ax = fabsf(x);
-    if (ax >= 0x1p-125f && ax <= 0x1p125f) {
-        const float r = __builtin_amdgcn_rcpf(x);
-        const float e = fmaf(-x, r, 1.0f);
-        return fmaf(e, r, r);
-    }
-    return 1.0f / x;
 }
 
 // Core/triangle.h:27-62 with edge1/edge2 precomputed (same IEEE subtraction, done once).
@@ -681,7 +666,10 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
             out_medium = -1;
         }
     }
-    v3 refr = refraction(normal, d, in_n, out_n);
+    // in_n / out_n and out_n / in_n: the material's two ratios, swapped when the ray leaves it
+    const float ratio_io = out_medium < 0 ? M.ratio_back : M.ratio_front;
+    const float ratio_oi = out_medium < 0 ? M.ratio_front : M.ratio_back;
+    v3 refr = refraction(normal, d, ratio_io);
     v3 bias_v = cfg.bias * normal;
 
     float R;
@@ -730,8 +718,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
         ps->o = point - bias_v;
         ps->d = refr;
         ps->medium = out_medium;
-        float ratio = out_n / in_n;
-        ps->thr = ps->thr * (ratio * ratio);
+        ps->thr = ps->thr * (ratio_oi * ratio_oi);  // ratio = out_n / in_n
     }
     mark(3);
     return length(ps->thr) > cfg.energy_threshold;

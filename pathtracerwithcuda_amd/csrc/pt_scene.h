@@ -54,8 +54,10 @@ struct alignas(16) DevMaterial {
     float rough_alpha;  // pow(roughness, 1.85) * 0.238 (path_tracer_kernel.cu:571)
     float tir_front;    // asin(n / air_n): fresnel.h:34 TIR threshold entering the material
     float tir_back;     // asin(air_n / n): the same leaving it (transparent back face)
+    float ratio_front;  // air_n / n: refraction's in_n / out_n entering (path_tracer_kernel.cu:60)
+    float ratio_back;   // n / air_n: the same leaving it
 };
-static_assert(sizeof(DevMaterial) == 96, "DevMaterial layout");
+static_assert(sizeof(DevMaterial) == 112, "DevMaterial layout");
 
 struct DevScene {
     const float4* nodes;
