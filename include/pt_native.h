@@ -25,6 +25,10 @@ extern "C" {
 typedef struct pt_context pt_context;
 
 const char* pt_last_error(void);
+/* Numerics helper: the largest float x >= 0 whose correctly rounded sqrtf is <= c (NaN for NaN, -1 when
+ * none). The kernels test length(v) > c as dot(v, v) > x (DevConfig: the kill and SSS thresholds and
+ * Fresnel's 0.000005f, path_tracer_kernel.cu:460,612-616, fresnel.h:37): the same outcome, no sqrt. */
+float pt_sqrt_le_bound(float c);
 int pt_device_count(void);
 
 int pt_context_create(int device, pt_context** out);

@@ -182,6 +182,7 @@ _PROTOS = {
     "thread_shrink": (C.c_int, [C.c_void_p, C.c_int]),
     # native (include/pt_native.h)
     "pt_last_error": (C.c_char_p, []),
+    "pt_sqrt_le_bound": (C.c_float, [C.c_float]),
     "pt_device_count": (C.c_int, []),
     "pt_context_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     "pt_context_destroy": (None, [C.c_void_p]),

@@ -517,8 +517,9 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 if (PT_DUP == 2) {
                     MeshWalk w2 = w; v3 o2 = ps.o, i2 = inv; int t2 = ptri;
                     opaque(w2); opaque(o2); opaque(i2);
-                    bool l2 = walk_box_chain<2>(rn, o2, i2, w2, t2);
-                    opaque(w2); opaque(l2); opaque(t2);
+                    float4 a2, b2, c2;
+                    bool l2 = walk_box_inline(rn, o2, i2, w2, t2, a2, b2, c2);
+                    opaque(w2); opaque(l2); opaque(t2); opaque(a2); opaque(b2); opaque(c2);
                 }
                 // a leaf whose box passes: the lane parks with its triangle, which came with the step's records
                 if (walk_box_inline(rn, ps.o, inv, w, ptri, pta, ptb, ptc)) mode = LANE_TRI;

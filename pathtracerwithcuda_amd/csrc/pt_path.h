@@ -148,11 +148,13 @@ __device__ __forceinline__ float ggx_g1(float roughness, v3 macro, v3 micro, v3 
 
 // Core/fresnel.h:11-49 (pow(x, 2.0f) -> x*x). tir_asin = asin(out_n / in_n), precomputed per material
 // (DevMaterial::tir_front / tir_back; only read when in_n > out_n).
-__device__ __forceinline__ float fresnel_dielectric(v3 n, v3 in, float in_n, float out_n, v3 refr, float tir_asin) {
+// refr_len2: DevConfig::refr_len2 (length(refr) <= 0.000005f as dot(refr, refr) <= refr_len2, exact).
+__device__ __forceinline__ float fresnel_dielectric(v3 n, v3 in, float in_n, float out_n, v3 refr, float tir_asin,
+                                                   float refr_len2) {
     float cos_in = dot(n, in * -1.0f);
     float cos_out = dot(-1.0f * n, refr);
     if (in_n > out_n && acos_pt(cos_in) >= tir_asin) return 1.0f;
-    if (length(refr) <= 0.000005f || cos_out < 0) return 1.0f;
+    if (dot(refr, refr) <= refr_len2 || cos_out < 0) return 1.0f;
     float s = (in_n * cos_in - out_n * cos_out) / (in_n * cos_in + out_n * cos_out);
     float p = (in_n * cos_out - out_n * cos_in) / (in_n * cos_out + out_n * cos_in);
     float rs = s * s;
@@ -597,7 +599,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
     if (FEAT & PT_FEAT_MEDIUM) {
         float sa[3], ss[3];
         medium_coefficients(sc, cfg, ps->medium, sa, ss);
-        if (ss[0] > 0.0f || length(mk3(sa[0], sa[1], sa[2])) > cfg.sss_threshold) {
+        if (ss[0] > 0.0f || dot(mk3(sa[0], sa[1], sa[2]), mk3(sa[0], sa[1], sa[2])) > cfg.sss_len2) {
             float r = minstd_uniform(&rng, 0.0f, 1.0f);
             float dist = -log_pt(r) / ss[0];
             if (dist < min_t) {
@@ -607,7 +609,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
                 ps->d = sample_sphere(r1, r2);
                 ps->thr = ps->thr * absorption(sa, dist);
                 if (STATS) ctr->scatter++;
-                return length(ps->thr) > cfg.energy_threshold;
+                return dot(ps->thr, ps->thr) > cfg.energy_len2;  // length(thr) > energy_threshold
             }
             ps->thr = ps->thr * absorption(sa, min_t);
         }
@@ -674,7 +676,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
 
     float R;
     const float k = M.extinction_coefficient;
-    if (k == 0 || transparent) R = fresnel_dielectric(normal, d, in_n, out_n, refr, out_medium < 0 ? M.tir_back : M.tir_front);
+    if (k == 0 || transparent) R = fresnel_dielectric(normal, d, in_n, out_n, refr, out_medium < 0 ? M.tir_back : M.tir_front, cfg.refr_len2);
     else R = fresnel_conductor(normal, d, out_n, k);
 
     mark(2);
@@ -721,7 +723,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
         ps->thr = ps->thr * (ratio_oi * ratio_oi);  // ratio = out_n / in_n
     }
     mark(3);
-    return length(ps->thr) > cfg.energy_threshold;
+    return dot(ps->thr, ps->thr) > cfg.energy_len2;  // length(thr) > energy_threshold
 }
 
 // pixel_256_transform_gamma_corrected_kernel (path_tracer_kernel.cu:627-682) for one pixel.

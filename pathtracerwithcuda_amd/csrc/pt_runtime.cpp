@@ -380,6 +380,20 @@ int translate_scene(SceneStage& st, int mesh_num, pt_bvh_node_device** bvh_nodes
     return PT_OK;
 }
 
+// The largest float x >= 0 with sqrtf(x) <= c (sqrtf correctly rounded, hence monotone): then
+// sqrtf(d) <= c exactly when d <= x, for every d >= 0 and NaN (NaN for a NaN c, -1 when no x exists).
+float sqrt_le_bound(float c) {
+    if (std::isnan(c)) return c;
+    if (!(sqrtf(0.0f) <= c)) return -1.0f;
+    uint32_t lo = 0, hi = 0x7f800000u;  // +0 .. +inf
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo + 1) / 2;
+        if (sqrtf(__builtin_bit_cast(float, mid)) <= c) lo = mid;
+        else hi = mid - 1;
+    }
+    return __builtin_bit_cast(float, lo);
+}
+
 DevConfig to_dev(const pt_configuration& c) {
     DevConfig d;
     d.max_depth = c.max_tracer_depth;
@@ -397,6 +411,9 @@ DevConfig to_dev(const pt_configuration& c) {
     d.air_reduced_scattering[0] = c.air_reduced_scattering_coef.x;
     d.air_reduced_scattering[1] = c.air_reduced_scattering_coef.y;
     d.air_reduced_scattering[2] = c.air_reduced_scattering_coef.z;
+    d.energy_len2 = sqrt_le_bound(d.energy_threshold);
+    d.sss_len2 = sqrt_le_bound(d.sss_threshold);
+    d.refr_len2 = sqrt_le_bound(0.000005f);
     return d;
 }
 
@@ -1179,6 +1196,8 @@ bool is_device_memory(const void* p) {
 // =============================================================================================
 // native C-ABI
 extern "C" const char* pt_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" float pt_sqrt_le_bound(float c) { return sqrt_le_bound(c); }
 
 extern "C" int pt_device_count(void) {
     int n = 0;

@@ -6,6 +6,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 
 import pathtracerwithcuda_amd as pt
 from pathtracerwithcuda_amd import _abi
@@ -77,3 +78,31 @@ def test_no_device_fails_loudly_without_gpu():
         assert "device" in str(e).lower()
     else:
         raise AssertionError("Renderer() succeeded without a device")
+
+
+@pytest.mark.filterwarnings("ignore::RuntimeWarning")  # float32 overflow of the 1e30 case's helpers
+@pytest.mark.parametrize("c", [0.000005, 0.0001, 0.01, 0.5, 1.0, 3.0e-20, 1.0e30, 0.0, -0.0, -1.0, float("inf"),
+                               float("nan")])
+def test_sqrt_le_bound_replaces_length_tests_exactly(c):
+    """pt_sqrt_le_bound(c) = the largest x >= 0 with sqrtf(x) <= c: the kernels test length(v) > c as
+    dot(v, v) > x. Checked at the boundary and on random squared lengths (numpy's float32 sqrt is the
+    correctly rounded sqrtf), NaN included."""
+    lib = pt.lib()
+    c32 = np.float32(c)
+    x = np.float32(lib.pt_sqrt_le_bound(float(c32)))
+    if np.isnan(c32):
+        assert np.isnan(x)
+        return
+    rng = np.random.default_rng(7)
+    d = np.concatenate([
+        rng.random(20000, dtype=np.float32) * np.float32(4) * max(np.float32(abs(c32)), np.float32(1e-30)) ** 2,
+        np.abs(rng.standard_normal(20000).astype(np.float32)),
+        np.array([0.0, np.inf, np.nan], dtype=np.float32),
+    ]).astype(np.float32)
+    if x >= 0:
+        near = np.array([np.nextafter(x, np.float32(-1)), x, np.nextafter(x, np.float32(np.inf))], dtype=np.float32)
+        d = np.concatenate([d, near[np.isfinite(near) & (near >= 0)]]).astype(np.float32)
+        assert np.sqrt(x) <= c32 and (np.isinf(x) or np.sqrt(np.nextafter(x, np.float32(np.inf))) > c32)
+    with np.errstate(invalid="ignore"):
+        assert np.array_equal(np.sqrt(d) > c32, d > x)
+        assert np.array_equal(np.sqrt(d) <= c32, d <= x)
