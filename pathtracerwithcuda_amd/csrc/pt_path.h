@@ -138,8 +138,13 @@ __device__ __forceinline__ float ggx_g1(float roughness, v3 macro, v3 micro, v3 
     v3 v = -1.0f * dir;
     float vdn = dot(v, macro);
     float vdm = dot(v, micro);
-    float positive = (vdm / vdn) > 0.0f ? 1.0f : 0.0f;
-    if (positive == 0.0f) return 0.0f;
+    // (vdm / vdn) > 0 without the division where its outcome is the operands' signs: for
+    // |vdm| >= 2^-100 and |vdn| <= 2^40 the quotient is neither NaN nor rounded to 0, and its sign is
+    // the XOR of the sign bits (a signed zero vdn included: x / +-0 = +-inf). Elsewhere, the division.
+    bool positive;
+    if (fabsf(vdm) >= 0x1p-100f && fabsf(vdn) <= 0x1p40f) positive = ((f2u(vdm) ^ f2u(vdn)) >> 31) == 0u;
+    else positive = (vdm / vdn) > 0.0f;
+    if (!positive) return 0.0f;
     float r2 = roughness * roughness;
     float c2 = vdn * vdn;
     float t2 = (1.0f - c2) / c2;
