@@ -428,16 +428,16 @@ __device__ __forceinline__ bool walk_box_inline(const __amdgpu_buffer_rsrc_t rn,
     const float4 lo0 = bload(rn, w.pos * 32), hi0 = bload(rn, w.pos * 32 + 16);
     const float4 lo1 = bload(rn, w.pos * 32 + 32), hi1 = bload(rn, w.pos * 32 + 48);
     asm volatile("" ::"v"(lo1.w), "v"(hi1.w));  // one round trip for all four loads (chain_load)
-    float entry;
+    // the triangle operands of a first-record leaf, assigned on every step (they are read only after a
+    // park): a conditional assignment makes the compiler merge old and new values through copies
     const int slot0 = f2i(hi0.w);
+    tri = slot0;
+    a = make_float4(lo1.x, lo1.y, lo1.z, 0.0f);
+    e1 = make_float4(lo1.w, hi1.x, hi1.y, 0.0f);
+    e2 = make_float4(hi1.z, hi1.w, lo0.w, 0.0f);
+    float entry;
     if (box_hit(lo0, hi0, o, inv, &entry) && entry <= w.t) {
-        if (slot0 >= 0) {
-            tri = slot0;
-            a = make_float4(lo1.x, lo1.y, lo1.z, 0.0f);
-            e1 = make_float4(lo1.w, hi1.x, hi1.y, 0.0f);
-            e2 = make_float4(hi1.z, hi1.w, lo0.w, 0.0f);
-            return true;
-        }
+        if (slot0 >= 0) return true;
         w.pos++;
         const int slot1 = f2i(hi1.w);
         if (box_hit(lo1, hi1, o, inv, &entry) && entry <= w.t) {
