@@ -188,7 +188,7 @@ enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3, LANE_T
 // rest from global memory (scenes of more than PT_LDS_MESHES meshes).
 #define PT_LDS_MESHES 64
 typedef int i32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ bool start_mesh(const DevScene& sc, const int2* lds_mesh, int& mesh, MeshWalk& w) {
+__device__ __forceinline__ bool start_mesh(const DevScene& sc, const int2* lds_mesh, int& mesh, int2& range) {
     while (mesh < sc.mesh_num) {
         int2 r;
         if (mesh < PT_LDS_MESHES) {
@@ -199,8 +199,7 @@ __device__ __forceinline__ bool start_mesh(const DevScene& sc, const int2* lds_m
             r.x = v.x; r.y = v.y;
         }
         if (r.x != r.y) {
-            w.pos = r.x; w.end = r.y;
-            w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
+            range = r;
             return true;
         }
         mesh++;
@@ -213,13 +212,17 @@ __device__ __forceinline__ bool start_mesh(const DevScene& sc, const int2* lds_m
 // start. One LDS read and no loop: a mesh change in a walk step then waits only on LDS, not on the wave's
 // outstanding vector loads (the looping version's mixed LDS / buffer-load path made it wait for every
 // one, parked lanes' triangle prefetches included).
-__device__ __forceinline__ bool start_mesh_next(const int4* lds_next, int& mesh, MeshWalk& w) {
+__device__ __forceinline__ bool start_mesh_next(const int4* lds_next, int& mesh, int2& range) {
     const int4 e = lds_next[mesh];
     mesh = e.z;
-    if (e.x == e.y) return false;
-    w.pos = e.x; w.end = e.y;
+    range = make_int2(e.x, e.y);
+    return e.x != e.y;
+}
+
+// A mesh walk's start state over node range r (the walk's local min_t starts at infinity).
+__device__ __forceinline__ void walk_start(MeshWalk& w, int2 r) {
+    w.pos = r.x; w.end = r.y;
     w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
-    return true;
 }
 
 // Start of one trace_ray_kernel invocation (path_tracer_kernel.cu:418-454): brute-force spheres into
@@ -237,8 +240,7 @@ __device__ __forceinline__ int begin_segment(const DevScene& sc, const PathState
     if (sc.first_mesh >= sc.mesh_num) return LANE_READY;  // (start_mesh from mesh 0, resolved on the host)
     inv = mk3(rcp_exact(ps.d.x), rcp_exact(ps.d.y), rcp_exact(ps.d.z));  // == 1.0f / d
     mesh = sc.first_mesh;
-    w.pos = sc.first_range.x; w.end = sc.first_range.y;
-    w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
+    walk_start(w, sc.first_range);
     return LANE_WALK;
 }
 
@@ -250,11 +252,9 @@ __device__ __forceinline__ int begin_segment(const DevScene& sc, const PathState
 // test with the same infinite min_t). `mesh` then holds the mesh being walked in bits 0-7 and the meshes
 // still to walk as a bit mask from bit 8 on (bit 8 + i: mesh i), so the skip costs no register.
 #define PT_ROOT_MESHES 24
-__device__ __forceinline__ void root_walk_start(const int2* lds_mesh, const float4* lds_root, int m, MeshWalk& w) {
+__device__ __forceinline__ int2 root_walk_range(const int2* lds_mesh, const float4* lds_root, int m) {
     const int2 r = lds_mesh[m];
-    w.pos = f2i(lds_root[2 * m + 1].w) < 0 ? r.x + 1 : r.x;  // below an internal root, at a leaf root
-    w.end = r.y;
-    w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
+    return make_int2(f2i(lds_root[2 * m + 1].w) < 0 ? r.x + 1 : r.x, r.y);  // below an internal root, at a leaf root
 }
 __device__ __forceinline__ int begin_segment_roots(const DevScene& sc, const int2* lds_mesh, const float4* lds_root,
                                                    const PathState& ps, v3& inv, Hit& h, MeshWalk& w, int& mesh) {
@@ -279,17 +279,16 @@ __device__ __forceinline__ int begin_segment_roots(const DevScene& sc, const int
     if (!todo) return LANE_READY;
     const int m = __builtin_ctz(todo);
     mesh = m | (int)((todo & (todo - 1u)) << 8);
-    root_walk_start(lds_mesh, lds_root, m, w);
+    walk_start(w, root_walk_range(lds_mesh, lds_root, m));
     return LANE_WALK;
 }
-// The next mesh of a root-masked segment (mesh_done): false when none is left.
-__device__ __forceinline__ bool next_root_mesh(const int2* lds_mesh, const float4* lds_root, int& mesh, MeshWalk& w) {
+// The next mesh of a root-masked segment (mesh_done) and its walk range: false when none is left.
+__device__ __forceinline__ bool next_root_mesh(const int2* lds_mesh, const float4* lds_root, int& mesh, int2& range) {
     const unsigned int rest = (unsigned int)mesh >> 8;
-    if (!rest) return false;
-    const int m = __builtin_ctz(rest);
+    const int m = rest ? __builtin_ctz(rest) : 0;
+    range = root_walk_range(lds_mesh, lds_root, m);
     mesh = m | (int)((rest & (rest - 1u)) << 8);
-    root_walk_start(lds_mesh, lds_root, m, w);
-    return true;
+    return rest != 0u;
 }
 
 // pixel_256_transform_gamma_corrected_kernel (:644-680) for one finished (pixel, pass) unit
@@ -486,13 +485,17 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 h.t = w.t; h.t1 = w.t1; h.t2 = w.t2; h.prim = w.tri; h.type = 2;
             }
             bool more;
+            int2 range = make_int2(0, 0);
             if (roots) {
-                more = next_root_mesh(lds_mesh, lds_root, mesh, w);
+                more = next_root_mesh(lds_mesh, lds_root, mesh, range);
             } else {
                 mesh++;
-                if (sc.mesh_num <= PT_LDS_MESHES) more = start_mesh_next(lds_next, mesh, w);
-                else more = start_mesh(sc, lds_mesh, mesh, w);
+                if (sc.mesh_num <= PT_LDS_MESHES) more = start_mesh_next(lds_next, mesh, range);
+                else more = start_mesh(sc, lds_mesh, mesh, range);
             }
+            // the walk state is reset whether or not a mesh is left (a READY lane does not read it), so
+            // the branches above only produce a range and the compiler merges no walk fields
+            walk_start(w, range);
             mode = more ? LANE_WALK : LANE_READY;
         };
         // the parked triangle's geometry, loaded at the park; scoped to the walk loop, which no lane leaves
