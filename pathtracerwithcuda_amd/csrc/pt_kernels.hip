@@ -225,25 +225,6 @@ __device__ __forceinline__ void walk_start(MeshWalk& w, int2 r) {
     w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
 }
 
-// Start of one trace_ray_kernel invocation (path_tracer_kernel.cu:418-454): brute-force spheres into
-// the closest hit, then the walk of the first mesh.
-__device__ __forceinline__ int begin_segment(const DevScene& sc, const PathState& ps, v3& inv, Hit& h, MeshWalk& w,
-                                             int& mesh) {
-    h.t = __builtin_inff(); h.t1 = __builtin_inff(); h.t2 = __builtin_inff();
-    h.type = 0; h.prim = -1;
-    for (int i = 0; i < sc.sphere_num; i++) {
-        float t;
-        if (sphere_t(sc.spheres[2 * i], ps.o, ps.d, &t) && t < h.t && t > 0.0f) {
-            h.t = t; h.prim = i; h.type = 1;
-        }
-    }
-    if (sc.first_mesh >= sc.mesh_num) return LANE_READY;  // (start_mesh from mesh 0, resolved on the host)
-    inv = mk3(rcp_exact(ps.d.x), rcp_exact(ps.d.y), rcp_exact(ps.d.z));  // == 1.0f / d
-    mesh = sc.first_mesh;
-    walk_start(w, sc.first_range);
-    return LANE_WALK;
-}
-
 // ---- root boxes at segment start (at most PT_ROOT_MESHES meshes) ----------------------------------
 // Each mesh's walk starts at its root with a local min_t of infinity (intersect_triangle_mesh_bvh,
 // :113-150), so a ray whose slab test fails on a mesh's root box gets nothing from that mesh. The roots of
@@ -256,8 +237,14 @@ __device__ __forceinline__ int2 root_walk_range(const int2* lds_mesh, const floa
     const int2 r = lds_mesh[m];
     return make_int2(f2i(lds_root[2 * m + 1].w) < 0 ? r.x + 1 : r.x, r.y);  // below an internal root, at a leaf root
 }
-__device__ __forceinline__ int begin_segment_roots(const DevScene& sc, const int2* lds_mesh, const float4* lds_root,
-                                                   const PathState& ps, v3& inv, Hit& h, MeshWalk& w, int& mesh) {
+
+// Start of one trace_ray_kernel invocation (path_tracer_kernel.cu:418-454): brute-force spheres into
+// the closest hit, then the walk of the first mesh (roots, wave-uniform: of the first mesh whose root box
+// the ray hits, from the LDS root table). Both ways produce only the first mesh and its node range, and
+// the walk state is set once from them, so the compiler merges no walk fields between the two.
+__device__ __forceinline__ int begin_segment(const DevScene& sc, bool roots, const int2* lds_mesh,
+                                             const float4* lds_root, const PathState& ps, v3& inv, Hit& h,
+                                             MeshWalk& w, int& mesh) {
     h.t = __builtin_inff(); h.t1 = __builtin_inff(); h.t2 = __builtin_inff();
     h.type = 0; h.prim = -1;
     for (int i = 0; i < sc.sphere_num; i++) {
@@ -266,21 +253,28 @@ __device__ __forceinline__ int begin_segment_roots(const DevScene& sc, const int
             h.t = t; h.prim = i; h.type = 1;
         }
     }
-    if (sc.first_mesh >= sc.mesh_num) return LANE_READY;
+    if (sc.first_mesh >= sc.mesh_num) return LANE_READY;  // (start_mesh from mesh 0, resolved on the host)
     inv = mk3(rcp_exact(ps.d.x), rcp_exact(ps.d.y), rcp_exact(ps.d.z));  // == 1.0f / d
-    unsigned int todo = 0;
-    for (int i = sc.first_mesh; i < sc.mesh_num; i++) {  // wave-uniform loop, broadcast LDS reads
-        const int2 r = lds_mesh[i];
-        if (r.x == r.y) continue;
-        float entry;
-        if (box_hit(lds_root[2 * i], lds_root[2 * i + 1], ps.o, inv, &entry) && entry <= __builtin_inff())
-            todo |= 1u << i;
+    int first = sc.first_mesh;
+    int2 range = sc.first_range;
+    bool any = true;
+    if (roots) {
+        unsigned int todo = 0;
+        for (int i = sc.first_mesh; i < sc.mesh_num; i++) {  // wave-uniform loop, broadcast LDS reads
+            const int2 r = lds_mesh[i];
+            if (r.x == r.y) continue;
+            float entry;
+            if (box_hit(lds_root[2 * i], lds_root[2 * i + 1], ps.o, inv, &entry) && entry <= __builtin_inff())
+                todo |= 1u << i;
+        }
+        any = todo != 0u;
+        const int m = any ? __builtin_ctz(todo) : 0;
+        first = m | (int)((todo & (todo - 1u)) << 8);
+        range = root_walk_range(lds_mesh, lds_root, m);
     }
-    if (!todo) return LANE_READY;
-    const int m = __builtin_ctz(todo);
-    mesh = m | (int)((todo & (todo - 1u)) << 8);
-    walk_start(w, root_walk_range(lds_mesh, lds_root, m));
-    return LANE_WALK;
+    mesh = first;
+    walk_start(w, range);
+    return any ? LANE_WALK : LANE_READY;
 }
 // The next mesh of a root-masked segment (mesh_done) and its walk range: false when none is left.
 __device__ __forceinline__ bool next_root_mesh(const int2* lds_mesh, const float4* lds_root, int& mesh, int2& range) {
@@ -348,7 +342,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 while (j < n && lds_mesh[j].x == lds_mesh[j].y) j++;
                 lds_next[i] = j < n ? make_int4(lds_mesh[j].x, lds_mesh[j].y, j, 0) : make_int4(0, 0, n, 0);
             }
-            if (n <= PT_ROOT_MESHES) {  // lds_root (begin_segment_roots)
+            if (n <= PT_ROOT_MESHES) {  // lds_root (begin_segment with roots)
                 const float4* nodes = uniform_ptr(P0->sc.nodes);
                 for (int i = threadIdx.x; i < 2 * n; i += PT_UBLOCK) {
                     const int2 r = lds_mesh[i >> 1];
@@ -440,8 +434,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             }
         }
         if (mode == LANE_NEW) {
-            if (roots) mode = begin_segment_roots(sc, lds_mesh, lds_root, ps, inv, h, w, mesh);
-            else mode = begin_segment(sc, ps, inv, h, w, mesh);
+            mode = begin_segment(sc, roots, lds_mesh, lds_root, ps, inv, h, w, mesh);
         }
         if (!__any(mode != LANE_DONE)) break;
         if (PROF) { const unsigned long long t = __builtin_readcyclecounter(); prof[8] += t - tc; tc = t; }
