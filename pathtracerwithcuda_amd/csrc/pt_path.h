@@ -693,13 +693,17 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
     float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
     float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
     if (reflect || !transparent) {
+        // both branches take sqrtf(r1) and one more square root: computed once for the batch, with the
+        // second one's argument chosen per lane (a batch holds lanes of both kinds)
+        const float s1 = sqrtf(r1);
+        const float s2 = sqrtf(reflect ? 1.0f - r1 : 1.0f - s1 * s1);
         float cos_t, sin_t;
         if (reflect) {  // sample_on_hemisphere_ggx_weight (:194-223), alpha = roughness^1.85 * 0.238 (:571)
-            const float theta = atan_pt(M.rough_alpha * sqrtf(r1) / sqrtf(1.0f - r1));
+            const float theta = atan_pt(M.rough_alpha * s1 / s2);  // alpha * sqrtf(r1) / sqrtf(1 - r1)
             sincos_pt(theta, &sin_t, &cos_t);
         } else {        // sample_on_hemisphere_cosine_weight (:163-192)
-            cos_t = sqrtf(r1);
-            sin_t = sqrtf(1.0f - cos_t * cos_t);
+            cos_t = s1;  // sqrtf(r1)
+            sin_t = s2;  // sqrtf(1 - cos_t * cos_t)
         }
         const v3 dir = hemisphere_dir(normal, cos_t, sin_t, r2);
         if (reflect) {  // reflection (:565-584)
