@@ -724,6 +724,7 @@ __global__ __launch_bounds__(PT_BLOCK) void math_eval_kernel(int which, const fl
         case 8: r0 = sqrtf(a); r1 = 1.0f / a; break;
         case 9: r0 = u8_unit((unsigned int)a); break;  // texel byte -> [0, 1] (texture.h:47-66)
         case 10: r0 = rcp_exact(a); r1 = 1.0f / a; break;
+        case 11: r0 = sqrt_exact(a); r1 = sqrtf(a); break;
         default: break;
     }
     o0[i] = r0;

@@ -54,8 +54,6 @@ PT_HD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 PT_HD v3 cross(v3 a, v3 b) {
     return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
-// cuda_math.hpp:1438
-PT_HD float length(v3 v) { return sqrtf(dot(v, v)); }
 #if defined(__HIPCC__)
 // 1.0f / x correctly rounded (the IEEE division of the reference and the oracle), from v_rcp_f32
 // (1 ulp) refined by one Newton step with an exact FMA residual: 3 instructions instead of the 10 of
@@ -71,12 +69,35 @@ __device__ __forceinline__ float rcp_exact(float x) {
     }
     return 1.0f / x;
 }
+// sqrtf(x) correctly rounded, for x in [2^-96, inf): v_sqrt_f32 (within 1 ulp) then the two one-ulp
+// residual checks of the compiler's own sqrtf expansion, without its scaling of small inputs and its
+// class test for 0 / inf / NaN, which that range does not need. Elsewhere sqrtf itself runs.
+// test_sqrt_exact_matches_sqrtf checks every significand at both exponent parities and the edges.
+__device__ __forceinline__ float sqrt_exact(float x) {
+    if (__float_as_uint(x) - 0x0f800000u < 0x70000000u) {  // 2^-96 <= x < inf
+        const float s = __builtin_amdgcn_sqrtf(x);
+        const float lo = __uint_as_float(__float_as_uint(s) - 1u), hi = __uint_as_float(__float_as_uint(s) + 1u);
+        const float r = fmaf(-lo, s, x) <= 0.0f ? lo : s;
+        return fmaf(-hi, s, x) > 0.0f ? hi : r;
+    }
+    return sqrtf(x);
+}
 #endif
+// sqrtf: sqrt_exact on the device (the same correctly rounded value), the libm call on the host
+PT_HD float sqrt_pt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return sqrt_exact(x);
+#else
+    return sqrtf(x);
+#endif
+}
+// cuda_math.hpp:1438
+PT_HD float length(v3 v) { return sqrt_pt(dot(v, v)); }
 // cuda_math.hpp:1458 (rsqrtf -> 1/sqrtf, see header; on the device the reciprocal is rcp_exact, the
 // same correctly rounded value)
 PT_HD v3 normalize(v3 v) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    float inv_len = rcp_exact(sqrtf(dot(v, v)));
+    float inv_len = rcp_exact(sqrt_exact(dot(v, v)));
 #else
     float inv_len = 1.0f / sqrtf(dot(v, v));
 #endif
@@ -183,7 +204,7 @@ PT_HD float asin_pt(float xx) {
     if (a < 1.0e-4f) return xx;
     float x, z;
     int flag;
-    if (a > 0.5f) { z = 0.5f * (1.0f - a); x = sqrtf(z); flag = 1; }
+    if (a > 0.5f) { z = 0.5f * (1.0f - a); x = sqrt_pt(z); flag = 1; }
     else { x = a; z = x * x; flag = 0; }
     z = ((((4.2163199048E-2f * z + 2.4181311049E-2f) * z + 4.5470025998E-2f) * z + 7.4953002686E-2f) * z
          + 1.6666752422E-1f) * z * x + x;
@@ -193,8 +214,8 @@ PT_HD float asin_pt(float xx) {
 PT_HD float acos_pt(float x) {
     if (x != x) return x;
     if (x < -1.0f || x > 1.0f) return u2f(0x7fc00000u);
-    if (x < -0.5f) return 3.14159265358979f - 2.0f * asin_pt(sqrtf(0.5f * (1.0f + x)));
-    if (x > 0.5f) return 2.0f * asin_pt(sqrtf(0.5f * (1.0f - x)));
+    if (x < -0.5f) return 3.14159265358979f - 2.0f * asin_pt(sqrt_pt(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * asin_pt(sqrt_pt(0.5f * (1.0f - x)));
     return kPIO2F - asin_pt(x);
 }
 

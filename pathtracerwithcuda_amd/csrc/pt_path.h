@@ -66,8 +66,8 @@ __device__ __forceinline__ v3 refraction(v3 n, v3 in, float ratio) {
     float a = ratio * ndi;
     float b = 1.0f - ratio * ratio * (1.0f - ndi * ndi);
     if (b < 0.0f) return mk3(0.0f, 0.0f, 0.0f);
-    if (ndi > 0) return n * (a - sqrtf(b)) - ratio * i;
-    return n * (a + sqrtf(b)) - ratio * i;
+    if (ndi > 0) return n * (a - sqrt_pt(b)) - ratio * i;
+    return n * (a + sqrt_pt(b)) - ratio * i;
 }
 
 // Orthonormal frame of sample_on_hemisphere_* (path_tracer_kernel.cu:175-189). The reference
@@ -95,8 +95,8 @@ __device__ __forceinline__ v3 hemisphere_dir(v3 n, float cos_theta, float sin_th
 
 // path_tracer_kernel.cu:163-192
 __device__ __forceinline__ v3 sample_cosine(v3 n, float r1, float r2) {
-    float cos_theta = sqrtf(r1);
-    float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+    float cos_theta = sqrt_pt(r1);
+    float sin_theta = sqrt_pt(1.0f - cos_theta * cos_theta);
     float phi = r2 * kTWO_PI;
     v3 vi, vj;
     tangent_frame(n, &vi, &vj);
@@ -107,7 +107,7 @@ __device__ __forceinline__ v3 sample_cosine(v3 n, float r1, float r2) {
 
 // path_tracer_kernel.cu:194-223
 __device__ __forceinline__ v3 sample_ggx(v3 n, float roughness, float r1, float r2) {
-    float theta = atan_pt(roughness * sqrtf(r1) / sqrtf(1.0f - r1));
+    float theta = atan_pt(roughness * sqrt_pt(r1) / sqrt_pt(1.0f - r1));
     float phi = r2 * kTWO_PI;
     float sin_theta, cos_theta;
     sincos_pt(theta, &sin_theta, &cos_theta);
@@ -121,7 +121,7 @@ __device__ __forceinline__ v3 sample_ggx(v3 n, float roughness, float r1, float 
 // path_tracer_kernel.cu:225-236
 __device__ __forceinline__ v3 sample_sphere(float r1, float r2) {
     float cos_theta = r1 * 2.0f - 1.0f;
-    float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+    float sin_theta = sqrt_pt(1.0f - cos_theta * cos_theta);
     float phi = r2 * kTWO_PI;
     float sp, cp;
     sincos_pt(phi, &sp, &cp);
@@ -148,7 +148,7 @@ __device__ __forceinline__ float ggx_g1(float roughness, v3 macro, v3 micro, v3 
     float r2 = roughness * roughness;
     float c2 = vdn * vdn;
     float t2 = (1.0f - c2) / c2;
-    return 2.0f / (1.0f + sqrtf(1.0f + r2 * t2));
+    return 2.0f / (1.0f + sqrt_pt(1.0f + r2 * t2));
 }
 
 // Core/fresnel.h:11-49 (pow(x, 2.0f) -> x*x). tir_asin = asin(out_n / in_n), precomputed per material
@@ -257,7 +257,7 @@ __device__ __forceinline__ bool sphere_t(float4 s, v3 o, v3 d, float* t_out) {
     float b = dot(op, d);
     float delta = b * b - dot(op, op) + s.w * s.w;
     if (delta < 0) return false;
-    float dr = sqrtf(delta);
+    float dr = sqrt_pt(delta);
     float t1 = b - dr;
     float t2 = b + dr;
     if (t1 < 0 && t2 < 0) return false;
@@ -510,7 +510,7 @@ __device__ __forceinline__ void generate_path(const DevCamera& cam, const DevCon
         float r1 = minstd_uniform(&rng, -0.5f, 0.5f) + 0.5f;
         float r2 = minstd_uniform(&rng, -0.5f, 0.5f) + 0.5f;
         float angle = r1 * kTWO_PI;
-        float dist = cam.aperture * sqrtf(r2);
+        float dist = cam.aperture * sqrt_pt(r2);
         float sa, ca;
         sincos_pt(angle, &sa, &ca);
         float ax = ca * dist;
@@ -695,8 +695,8 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
     if (reflect || !transparent) {
         // both branches take sqrtf(r1) and one more square root: computed once for the batch, with the
         // second one's argument chosen per lane (a batch holds lanes of both kinds)
-        const float s1 = sqrtf(r1);
-        const float s2 = sqrtf(reflect ? 1.0f - r1 : 1.0f - s1 * s1);
+        const float s1 = sqrt_pt(r1);
+        const float s2 = sqrt_pt(reflect ? 1.0f - r1 : 1.0f - s1 * s1);
         float cos_t, sin_t;
         if (reflect) {  // sample_on_hemisphere_ggx_weight (:194-223), alpha = roughness^1.85 * 0.238 (:571)
             const float theta = atan_pt(M.rough_alpha * s1 / s2);  // alpha * sqrtf(r1) / sqrtf(1 - r1)

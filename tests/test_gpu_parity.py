@@ -100,6 +100,24 @@ def test_rcp_exact_matches_division(gpu):
     assert same.all(), f"{(~same).sum()} mismatches, e.g. x={x[~same][:4]} fast={fast[~same][:4]} div={div[~same][:4]}"
 
 
+def test_sqrt_exact_matches_sqrtf(gpu):
+    """sqrt_exact (v_sqrt_f32 + the two one-ulp residual checks, no scaling or class test on [2^-96, inf))
+    against the compiler's correctly rounded sqrtf on the device: every significand at both exponent
+    parities, at the guarded range's lower end and high up, plus the edges on either side of the guard."""
+    sig = (np.arange(1 << 23, dtype=np.uint32) | np.uint32(127 << 23)).view(np.float32)
+    xs = [sig * np.float32(2.0 ** e) for e in (0, 1, -96, -95, 100, 127)]
+    xs.append(np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-40, -1e-40, -1.0, 2.0 ** -96, 2.0 ** -97,
+                        np.nextafter(np.float32(2.0 ** -96), np.float32(0)), 3.4028235e38, 1.2e-38], np.float32))
+    x = np.concatenate(xs).astype(np.float32)
+    fast, ref = gpu.math_eval_device(11, x)
+    same = (fast.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(fast) & np.isnan(ref))
+    assert same.all(), f"{(~same).sum()} mismatches, e.g. x={x[~same][:4]} fast={fast[~same][:4]} ref={ref[~same][:4]}"
+    with np.errstate(invalid="ignore"):
+        host = np.sqrt(x)
+    same = (ref.view(np.uint32) == host.view(np.uint32)) | (np.isnan(ref) & np.isnan(host))
+    assert same.all(), "the device sqrtf is not the correctly rounded square root"
+
+
 def test_config1_spheres_only_cornell(gpu):
     sc = pt.cornell_spheres_scene(cube_length=64)
     cfg = pt.configuration(max_tracer_depth=4)
