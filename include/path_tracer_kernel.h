@@ -18,8 +18,9 @@
  * Differences a caller may observe:
  *   - scene pointers must be host-readable (the reference hands out cudaMallocManaged memory,
  *     which is). The scene is translated into the device layout of DESIGN.md §Data layout and
- *     cached; it is re-translated whenever pass_counter == 1 (the reference caller resets the
- *     pass counter after every scene edit, Core/path_tracer.cpp:101-107) or a pointer changes.
+ *     cached. On pass_counter == 1 (the reference caller resets the pass counter after every
+ *     scene edit, Core/path_tracer.cpp:101-107) the caller's scene bytes are hashed, and a
+ *     changed digest or pointer re-translates and re-uploads them.
  *   - the per-pixel scratch (not_absorbed / accumulated / rays / energy_exist_pixels /
  *     scatterings) is accepted and ignored: path state lives in registers. memory_allocate
  *     still returns buffers of the reference sizes, allocated as the reference allocates them:

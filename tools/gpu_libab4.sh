@@ -18,6 +18,6 @@ python3 - "$TAG" "$@" <<'PY'
 import json, sys, glob, statistics as st
 tag, dirs = sys.argv[1], sys.argv[2:]
 for d in dirs:
-    v = [json.load(open(f)) for f in sorted(glob.glob(f"gpurun_out/{tag}/bench_{d}_*.json"))]
+    v = [json.load(open(f)) for f in sorted(glob.glob(f"gpurun_out/{tag}/bench_{d}_[0-9]*.json"))]
     print(f"{d:12s} median {st.median(x['value'] for x in v):9.1f} Mrays/s  launch {st.median(x['roofline']['avg_launch_ms'] for x in v):.4f} ms")
 PY
