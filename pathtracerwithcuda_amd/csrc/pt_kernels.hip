@@ -440,7 +440,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         if (PROF) { const unsigned long long t = __builtin_readcyclecounter(); prof[8] += t - tc; tc = t; }
 
         const unsigned long long ready = __ballot(mode == LANE_READY);
-        const unsigned long long walking = __ballot(mode == LANE_WALK || mode == LANE_TRI);
+        const unsigned long long walking = __ballot(mode == LANE_WALK) | __ballot(mode == LANE_TRI);
         if (ready && (__popcll(walking) <= (unsigned int)walk_min || __popcll(ready) >= (unsigned int)shade_min)) {
             if (PROF) { prof[3]++; prof[4] += (unsigned long long)__popcll(ready); }
             if (PROF && drained) tail_segments += (unsigned long long)__popcll(ready);
@@ -495,7 +495,9 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         // parked (the last step flushes the batch), so it is not live across shading
         float4 pta = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ptb = pta, ptc = pta;
         for (int k = 0; k < walk_steps; k++) {
-            if (k > 0 && !__any(mode == LANE_WALK || mode == LANE_TRI)) break;
+            // two ballots, not one of (WALK || TRI): the compiler materialises an OR'ed predicate as a 0/1 VGPR
+            // and compares it again (two VALU more per step)
+            if (k > 0 && (__ballot(mode == LANE_WALK) | __ballot(mode == LANE_TRI)) == 0ull) break;
             if (PROF) {
                 prof[1]++; prof[2] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK));
                 prof[12] += (unsigned long long)__popcll(__ballot(mode == LANE_TRI));
