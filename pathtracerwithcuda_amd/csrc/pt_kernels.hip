@@ -645,6 +645,7 @@ __global__ __launch_bounds__(PT_BLOCK) void material_consts_kernel(DevMaterial* 
     m.ratio_back = m.refraction_index / air_n;
     m.tir_front = asin_pt(m.ratio_back);
     m.tir_back = asin_pt(m.ratio_front);
+    m.spec_zero = m.specular[0] == 0.0f && m.specular[1] == 0.0f && m.specular[2] == 0.0f;
 }
 
 hipError_t launch_material_consts(DevMaterial* mats, int n, float air_n, hipStream_t stream) {

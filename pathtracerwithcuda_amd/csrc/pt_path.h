@@ -693,6 +693,11 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
     float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
     float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
     if (reflect || !transparent) {
+        // A reflection off a material whose specular colour is (0, 0, 0) leaves thr * (spec * shadow) = 0 (or NaN
+        // where thr is infinite), whatever the sampled direction: the kill test (:612-616) ends the path with its
+        // radiance untouched (the reflect branch adds none), so the GGX sample is not computed. Not when the
+        // configured energy bound is negative (or NaN), where a zero throughput would survive the test.
+        if (reflect && M.spec_zero && cfg.energy_len2 >= 0.0f) return false;
         // both branches take sqrtf(r1) and one more square root: computed once for the batch, with the
         // second one's argument chosen per lane (a batch holds lanes of both kinds)
         const float s1 = sqrt_pt(r1);

@@ -56,6 +56,7 @@ struct alignas(16) DevMaterial {
     float tir_back;     // asin(air_n / n): the same leaving it (transparent back face)
     float ratio_front;  // air_n / n: refraction's in_n / out_n entering (path_tracer_kernel.cu:60)
     float ratio_back;   // n / air_n: the same leaving it
+    int spec_zero;      // specular == (0, 0, 0): a reflection's throughput is thr * (0 * shadow) (shade_hit)
 };
 static_assert(sizeof(DevMaterial) == 112, "DevMaterial layout");
 
