@@ -12,7 +12,7 @@ next frames' work (PT_BENCH_INFLIGHT=1:
 one at a time on the whole grid); the host-synchronised single-frame latency is reported beside it. Mrays/s = ray segments traced (the live-ray counts the
 reference's thread_shrink returns, summed over passes and depths and over ranks) / wall time.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]   (defaults: 20 timed frames after 5, C4/C5 3 after 1)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 """
 from __future__ import annotations
@@ -192,8 +192,10 @@ def load_profile(workload: str) -> dict:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    # defaults: the driver's 20 timed frames after 5 warm-up frames for the 1080p workloads (0.13 s of GPU time
+    # at the metric frame), 3 after 1 for the heavy C4/C5 frames
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--save-image", default="")
@@ -202,6 +204,11 @@ def main() -> int:
     ap.add_argument("--workload", choices=["metric", "c2", "c3", "c4", "c5"], default="metric",
                     help="metric: BASELINE.json's metric configuration (default); c3-c5: its heavier configs")
     args = ap.parse_args()
+    heavy = args.workload in ("c4", "c5")
+    if args.steps is None:
+        args.steps = 3 if heavy else 20
+    if args.warmup is None:
+        args.warmup = 1 if heavy else 5
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
