@@ -28,6 +28,8 @@ bool pass_uses_unified(const PassChoice& pc, int lds_bytes);
 // inline-leaf copy of the node array for pass_kernel_u (pt_kernels.hip inline_leaves_kernel)
 hipError_t launch_inline_leaves(const float4* nodes, const float4* tri_geom, const int* np, int R, float4* out,
                                 hipStream_t stream);
+// the cube map's RGBA8 texels as float4 {u8_unit(r), u8_unit(g), u8_unit(b), 0} (DevScene::cube_f)
+hipError_t launch_cube_float(const uint8_t* cube, int texels, float4* out, hipStream_t stream);
 hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int first_pass, int batch_log2,
                        int write_u8, int grid, int lds_bytes, hipStream_t stream);
 hipError_t launch_accumulate(const LaunchParams* params_dev, int units, int first_pass, int batch_log2, int write_u8,

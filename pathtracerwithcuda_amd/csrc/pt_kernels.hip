@@ -897,6 +897,21 @@ __global__ void inline_leaves_kernel(const float4* __restrict__ nodes, const flo
     }
 }
 
+__global__ __launch_bounds__(PT_BLOCK) void cube_float_kernel(const uint8_t* __restrict__ cube, int texels,
+                                                              float4* __restrict__ out) {
+    const int i = blockIdx.x * PT_BLOCK + threadIdx.x;
+    if (i >= texels) return;
+    const unsigned int t = texel_raw(cube, i);
+    out[i] = make_float4(texel_c(t, 0), texel_c(t, 1), texel_c(t, 2), 0.0f);
+}
+
+hipError_t launch_cube_float(const uint8_t* cube, int texels, float4* out, hipStream_t stream) {
+    if (texels <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cube_float_kernel, dim3((texels + PT_BLOCK - 1) / PT_BLOCK), dim3(PT_BLOCK), 0, stream, cube,
+                       texels, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_inline_leaves(const float4* nodes, const float4* tri_geom, const int* np, int R, float4* out,
                                 hipStream_t stream) {
     if (R <= 0) return hipSuccess;

@@ -224,6 +224,29 @@ __device__ __forceinline__ v3 sample_rgba8(const uint8_t* px, int w, int h, floa
     return mk3(texel_c(t, 0), texel_c(t, 1), texel_c(t, 2));
 }
 
+// sample_rgba8 on texels already converted to floats (DevScene::cube_f): the same index arithmetic and
+// lerps on the same values, without the per-sample byte conversions.
+__device__ __forceinline__ v3 sample_f4(const float4* px, int w, int h, float au, float av, int bilinear) {
+    if (bilinear) {
+        float xr = au * (float)(w - 1);
+        float yr = (1.0f - av) * (float)(h - 1);
+        int fx = (int)clampf(floorf(xr), 0.0f, (float)(w - 1));
+        int cx = (int)clampf(ceilf(xr), 0.0f, (float)(w - 1));
+        int fy = (int)clampf(floorf(yr), 0.0f, (float)(h - 1));
+        int cy = (int)clampf(ceilf(yr), 0.0f, (float)(h - 1));
+        float lr = xr - floorf(xr);
+        float bt = yr - floorf(yr);
+        const float4 t0 = px[fy * w + fx], t1 = px[fy * w + cx], t2 = px[cy * w + fx], t3 = px[cy * w + cx];
+        return mk3(lerp1(lerp1(t0.x, t1.x, lr), lerp1(t2.x, t3.x, lr), bt),
+                   lerp1(lerp1(t0.y, t1.y, lr), lerp1(t2.y, t3.y, lr), bt),
+                   lerp1(lerp1(t0.z, t1.z, lr), lerp1(t2.z, t3.z, lr), bt));
+    }
+    int x = (int)clampf(au * (float)(w - 1), 0.0f, (float)(w - 1));
+    int y = (int)clampf((1.0f - av) * (float)(h - 1), 0.0f, (float)(h - 1));
+    const float4 t = px[y * w + x];
+    return mk3(t.x, t.y, t.z);
+}
+
 __device__ __forceinline__ v3 sample_texture(const DevScene& sc, int id, v2 uv, int bilinear) {
     int4 d = sc.tex_desc[id];
     float au = uv.x - floorf(uv.x);
@@ -239,6 +262,7 @@ __device__ __forceinline__ v3 background(const DevScene& sc, const DevConfig& cf
         int face;
         xyz_to_cube_uv(d.x, d.y, d.z, &face, &u, &v);
         int len = sc.cube_len;
+        if (sc.cube_f) return sample_f4(sc.cube_f + (size_t)face * (size_t)len * (size_t)len, len, len, u, v, cfg.use_bilinear);
         const uint8_t* px = sc.cube + (size_t)face * (size_t)len * (size_t)len * 4;
         return sample_rgba8(px, len, len, u, v, cfg.use_bilinear);
     }

@@ -526,6 +526,7 @@ struct pt_context {
     // one triangle per leaf: the inline-leaf node array pass_kernel_u walks (pt_path.h walk_box_inline),
     // the record map it is built through (np, R + 1 ints), its mesh ranges and first range
     void* il_mem = nullptr;
+    void* cube_f_mem = nullptr;  // DevScene::cube_f
     const float4* il_nodes = nullptr;
     const int* il_np = nullptr;
     const int2* il_range = nullptr;
@@ -558,6 +559,9 @@ void free_scene(pt_context* ctx) {
     free_refit(ctx);
     if (ctx->il_mem) (void)hipFree(ctx->il_mem);
     ctx->il_mem = nullptr;
+    if (ctx->cube_f_mem) (void)hipFree(ctx->cube_f_mem);
+    ctx->cube_f_mem = nullptr;
+    ctx->scene.cube_f = nullptr;
     ctx->il_nodes = nullptr;
     ctx->il_np = nullptr;
     ctx->il_range = nullptr;
@@ -657,6 +661,13 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
             break;
         }
     s.nested = nested;
+    s.cube_f = nullptr;
+    if (st.cube_len > 0) {
+        const int texels = 6 * st.cube_len * st.cube_len;
+        PT_HIP(hipMalloc(&ctx->cube_f_mem, (size_t)texels * sizeof(float4)));
+        PT_HIP(launch_cube_float(s.cube, texels, (float4*)ctx->cube_f_mem, ctx->stream));
+        s.cube_f = (const float4*)ctx->cube_f_mem;
+    }
     ctx->node_num = (int)(st.nodes.size() / 2);
     ctx->mesh_range = st.mesh_range;
     ctx->tri_num = (int)(st.tri_geom.size() / 3);

@@ -81,6 +81,9 @@ struct DevScene {
     int first_mesh;    // first mesh with a non-empty node range (mesh_num if none) and that range:
     int2 first_range;  //   where every trace step's mesh walk starts
     int nested;        // 1: every node's box contains its children's boxes
+    // the cube map's texels as floats {b / 255} per channel (u8_unit, the same values the RGBA8 lookup
+    // computes per sample), 6 faces back to back like `cube`; null: the lookup converts the bytes
+    const float4* cube_f;
 };
 
 // The subset of Core/configuration.h:9-34 that the kernel reads.
