@@ -248,12 +248,13 @@ def main() -> int:
     # Each launch takes 1 / (F - 1) of the occupancy-sized grid (pt_set_grid_share). Measured best
     # (profiles/r02/scaling/hw_queues.txt, ms per frame of rank 0's share): three frames on half grids
     # for the whole frame (6.04 vs 6.13 with five), five on quarter grids for a tiled share (0.99 vs 1.08
-    # at N = 8, 1.76 vs 1.80 at N = 4, 3.24 vs 3.26 at N = 2). At N = 1 the two running launches take 45 % each
-    # rather than half: the queued third frame's first waves then start beside them (+0.27 %, 3 of 3 rounds,
-    # profiles/r03/grid_share/)
+    # at N = 8, 1.76 vs 1.80 at N = 4, 3.24 vs 3.26 at N = 2). At N = 1 the two running launches of a 1080p
+    # frame take 45 % each rather than half: the queued third frame's first waves then start beside them
+    # (+0.27 %, 3 of 3 rounds, profiles/r03/grid_share/). Not for the 0.4-4 s C4/C5 frames, whose tails are
+    # a small part of them: there the 10 % left to the third frame sits idle (C4 -3.8 %)
     inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or (3 if world == 1 else 5)
     grid_share = int(os.environ.get("PT_BENCH_GRID_SHARE", "0")) or (
-        (45 if inflight == 3 else 100 // (inflight - 1)) if inflight >= 3 else 100)
+        (45 if inflight == 3 and not heavy else 100 // (inflight - 1)) if inflight >= 3 else 100)
     wl = Workload(args.workload)
     scene, cfg, cam = wl.scene, wl.cfg, wl.cam
     width, height, spp = wl.width, wl.height, wl.spp
