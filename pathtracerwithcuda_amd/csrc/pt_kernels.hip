@@ -922,11 +922,12 @@ hipError_t launch_inline_leaves(const float4* nodes, const float4* tri_geom, con
 hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int first_pass, int batch_log2,
                        int write_u8, int grid, int lds_bytes, hipStream_t stream) {
     if (use_unified(pc.leaf1, pc.stats, lds_bytes)) {
-        // 64-unit chunks, a 28-lane shading batch, 8 walk steps per round, triangle batches of 6 lanes:
-        // measured best with frames in flight
+        // 64-unit chunks, a 28-lane shading batch, 7 walk steps per round, triangle batches of 6 lanes:
+        // measured best with frames in flight (7 steps since the end of round 3: metric
+        // +0.4 %, C3 +0.9 %, C4/C5 +0.1-0.3 %, profiles/r03/walk_steps/)
         static const int chunk = env_int("PT_CHUNK_MEGA", 64, 0, 4096);
         static const int shade_min = env_int("PT_SHADE_MIN", 28, 1, 64);
-        static const int walk_steps = env_int("PT_WALK_STEPS", 8, 1, 64);
+        static const int walk_steps = env_int("PT_WALK_STEPS", 7, 1, 64);
         static const int tri_min = env_int("PT_TRI_MIN", 6, 1, 64);
         static const int walk_min = env_int("PT_WALK_MIN", 8, 0, 64);
         int fu, wu;
