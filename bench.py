@@ -227,6 +227,11 @@ def main() -> int:
     # instead of queueing behind a persistent pass launch (16 and 8 measured equal for the share itself)
     hw_queues = os.environ.get("PT_BENCH_HW_QUEUES", "16" if world > 1 else "8")
     os.environ["GPU_MAX_HW_QUEUES"] = hw_queues
+    # Tiled shares batch triangle tests from 3 parked lanes instead of 6: a small share spends most of its
+    # launch in the tail, where few lanes walk (8-way share 0.869-0.871 vs 0.887-0.897 ms; at N = 1 it is
+    # -0.2 %, so the library default stays 6; profiles/r03/scaling/share8_knobs.txt)
+    if world > 1:
+        os.environ.setdefault("PT_TRI_MIN", "3")
     import torch
     import torch.distributed as dist
 
