@@ -86,6 +86,14 @@ class Workload:
             self.desc = ("Cornell box (cornell.obj walls, cube.obj light, iron+glass spheres) + torus knot, "
                          f"{self.scene.triangle_count} triangles, {self.scene.view.sphere_num} spheres")
             self.data = "synthetic: procedural 70k-triangle torus knot (bunny stand-in) + procedural 512^2 cube map"
+        elif name == "c1":  # BASELINE.json configs[0]: spheres-only Cornell box, 512x512, 4 spp, 4 bounces
+            self.width, self.height, self.spp, self.depth = 512, 512, 4, 4
+            self.scene = pt.cornell_spheres_scene()
+            cam_kw = dict(pitch=0.05, radius=11.0, center=(0.0, 1.2, 0.0))  # inside the box
+            self.key = "c1_cornell_spheres_512x512_spp4_d4"
+            self.desc = ("cornell_box_simple.json without meshes: five r=1000 wall spheres, a light sphere, iron + "
+                         f"glass spheres ({self.scene.view.sphere_num} spheres, no BVH)")
+            self.data = "synthetic: spheres-only Cornell box (cornell_box_simple.json materials) + procedural 512^2 cube map"
         elif name == "c2":  # Cornell + ~70k-triangle mesh, diffuse only, 1280x720
             self.width, self.height, self.spp, self.depth = 1280, 720, 8, 8
             self.scene = pt.cornell_scene(pt.torus_knot(*KNOT), mesh_material="diffuse_white", spheres=False)
@@ -145,20 +153,21 @@ class Workload:
         self.cam = pt.camera(self.width, self.height, **cam_kw)
 
 
-def cpu_baseline(scene, cam, cfg, threads: int) -> dict:
+def cpu_baseline(wl: "Workload", threads: int) -> dict:
     """The reference's CPU fallback semantics (Core/path_tracer_cpu.cpp: MSVC rand, libm), as
-    restated by the oracle, on the same frame: one whole frame (all 8 passes), so ms/frame is measured,
+    restated by the oracle, on the same frame: one whole frame (all of its passes), so ms/frame is measured,
     not extrapolated."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # cpu_baseline leg only
 
     oracle.lib()
     t0 = time.perf_counter()
-    _, _, st = oracle.render(scene.view, cam, cfg, 1, SPP, rng="msvc", math="libm", threads=threads, with_u8=True)
+    _, _, st = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, wl.spp, rng="msvc", math="libm", threads=threads,
+                             with_u8=True)
     dt = time.perf_counter() - t0
     return {"value": round(st["segments"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"one whole {WIDTH}x{HEIGHT} {SPP}-spp depth-{DEPTH} frame ({st['segments']} ray segments, "
-                      f"{dt:.2f} s), oracle in reference-CPU-fallback mode (MSVC rand, libm), OpenMP",
+            "sample": f"one whole {wl.width}x{wl.height} {wl.spp}-spp depth-{wl.depth} frame ({st['segments']} ray "
+                      f"segments, {dt:.2f} s), oracle in reference-CPU-fallback mode (MSVC rand, libm), OpenMP",
             "ms_per_frame": round(dt * 1000, 1)}
 
 
@@ -201,8 +210,9 @@ def main() -> int:
     ap.add_argument("--save-image", default="")
     ap.add_argument("--schedule", choices=["persistent", "wavefront"], default=None,
                     help="kernel schedule (default: the library's, PT_MODE)")
-    ap.add_argument("--workload", choices=["metric", "c2", "c3", "c4", "c5"], default="metric",
-                    help="metric: BASELINE.json's metric configuration (default); c3-c5: its heavier configs")
+    ap.add_argument("--workload", choices=["metric", "c1", "c2", "c3", "c4", "c5"], default="metric",
+                    help="metric: BASELINE.json's metric configuration (default); c1: its CPU-path plumbing config "
+                         "(the line then carries that frame's CPU-path time as cpu_baseline); c2-c5: its other configs")
     args = ap.parse_args()
     heavy = args.workload in ("c4", "c5")
     if args.steps is None:
@@ -455,9 +465,9 @@ def main() -> int:
         },
         "cpu_baseline": None,
     }
-    if world == 1 and not args.no_cpu_baseline and args.workload == "metric":
+    if world == 1 and not args.no_cpu_baseline and args.workload in ("metric", "c1"):
         threads, why = host_threads(args.cpu_threads)
-        line["cpu_baseline"] = cpu_baseline(scene, cam, cfg, threads)
+        line["cpu_baseline"] = cpu_baseline(wl, threads)
         line["cpu_baseline"]["cpu"] = platform.processor() or platform.machine()
         line["cpu_baseline"]["threads_from"] = why
     print(json.dumps(line), flush=True)

@@ -116,7 +116,9 @@ typedef struct {
     int math;
 } or_scene;
 
-typedef struct { unsigned long long nodes, tris; } or_counts;
+/* nan: segments whose kill test saw a NaN throughput length and, as the reference does (NaN <= x is false),
+ * kept the path (reported so a test can show that its scene reaches that case) */
+typedef struct { unsigned long long nodes, tris, nan; } or_counts;
 
 /* path_tracer_kernel.cu:46-52 */
 static or_v3 reflection(or_v3 n, or_v3 in) { return v_sub(in, s_scale(2.0f * v_dot(n, in), n)); }
@@ -467,7 +469,9 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
             st->rays[k].origin = pf3(v_add(o, v_scale(d, dist)));
             st->rays[k].direction = pf3(on_sphere(mm, r1, r2));
             st->thr[k] = v_mul(st->thr[k], absorption_through(mm, cs.absorption_coefficient, dist));
-            if (v_len(st->thr[k]) <= cfg->energy_exist_threshold) st->alive[ai] = -1;
+            float len = v_len(st->thr[k]);
+            if (len <= cfg->energy_exist_threshold) st->alive[ai] = -1;
+            else if (len != len) cnt->nan++;
             return;
         }
         st->thr[k] = v_mul(st->thr[k], absorption_through(mm, cs.absorption_coefficient, min_t));
@@ -557,7 +561,9 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
         st->rays[k].origin = pf3(v_add(min_point, bias));
         st->rays[k].direction = pf3(hemisphere_cosine(mm, min_normal, r1, r2));
     }
-    if (v_len(st->thr[k]) <= cfg->energy_exist_threshold) { st->alive[ai] = -1; sig_add(st, k, 5); }
+    float len = v_len(st->thr[k]);
+    if (len <= cfg->energy_exist_threshold) { st->alive[ai] = -1; sig_add(st, k, 5); }
+    else if (len != len) cnt->nan++;
 }
 
 /* thread_shrink: stable remove_if(v < 0) (parallel_function.cu:42-49) */
@@ -583,8 +589,9 @@ static void gamma_u8(int mm, const pt_configuration* cfg, const float* img, int 
 /*
  * Render passes first_pass .. first_pass+pass_count-1 for `n` pixels: pixel_list[k] (or k when
  * pixel_list is NULL). image (n*3 floats) and image256 (n*3 bytes, may be NULL) are the running
- * sum and 8-bit value of entry k, with the reference's pass_counter semantics. stats[0..2] (may be
- * NULL) receive ray segments, BVH nodes visited and triangle tests. Returns 0 or -1 (alloc).
+ * sum and 8-bit value of entry k, with the reference's pass_counter semantics. stats[0..3] (may be
+ * NULL) receive ray segments, BVH nodes visited, triangle tests and NaN-throughput survivals.
+ * Returns 0 or -1 (alloc).
  */
 int or_render_sig(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangle* triangles, int sphere_num,
                   const pt_sphere* spheres, const pt_cube_map* cube, const pt_texture_wrapper* textures,
@@ -612,7 +619,7 @@ int or_render_sig(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangl
 #else
     (void)threads;
 #endif
-    unsigned long long segs = 0, nodes = 0, tris = 0;
+    unsigned long long segs = 0, nodes = 0, tris = 0, nans = 0;
     for (int pass = first_pass; pass < first_pass + pass_count; pass++) {
         int seed = pass;
         #pragma omp parallel for schedule(dynamic, 256)
@@ -621,16 +628,18 @@ int or_render_sig(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangl
         for (int depth = 0; depth < cfg->max_tracer_depth; depth++) {
             if (count == 0) break;
             segs += (unsigned long long)count;
-            unsigned long long dn = 0, dt = 0;
-            #pragma omp parallel for schedule(dynamic, 256) reduction(+ : dn, dt)
+            unsigned long long dn = 0, dt = 0, dnan = 0;
+            #pragma omp parallel for schedule(dynamic, 256) reduction(+ : dn, dt, dnan)
             for (int ai = 0; ai < count; ai++) {
-                or_counts c = {0, 0};
+                or_counts c = {0, 0, 0};
                 trace(&sc, rng_kind, seed, depth, pixel_list, ai, &st, &c);
                 dn += c.nodes;
                 dt += c.tris;
+                dnan += c.nan;
             }
             nodes += dn;
             tris += dt;
+            nans += dnan;
             count = shrink(st.alive, count);
         }
         float hi = (float)cfg->max_tracer_depth * 2.0f;
@@ -647,7 +656,7 @@ int or_render_sig(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangl
             if (sigs) sigs[(size_t)(pass - first_pass) * n + k] = st.sig[k];
         }
     }
-    if (stats) { stats[0] = segs; stats[1] = nodes; stats[2] = tris; }
+    if (stats) { stats[0] = segs; stats[1] = nodes; stats[2] = tris; stats[3] = nans; }
     free(st.alive); free(st.rays); free(st.thr); free(st.rad); free(st.sca); free(st.sig);
     return 0;
 }

@@ -86,7 +86,7 @@ def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.
         img8 = image256.reshape(n, 3)
     else:
         img8 = np.zeros((n, 3), np.uint8) if with_u8 else None
-    stats = (C.c_ulonglong * 3)()
+    stats = (C.c_ulonglong * 4)()
     sigs = np.zeros((pass_count, n), np.uint64) if signatures else None
     rc = L.or_render_sig(view.mesh_num, C.cast(view.bvh_nodes, C.c_void_p), C.cast(view.triangles, C.c_void_p),
                      view.sphere_num, C.cast(view.spheres, C.c_void_p), C.cast(view.sky_cube_map, C.c_void_p),
@@ -96,7 +96,7 @@ def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.
                      sigs.ctypes.data if sigs is not None else None)
     if rc != 0:
         raise MemoryError("oracle allocation failed")
-    st = {"segments": stats[0], "nodes": stats[1], "tris": stats[2]}
+    st = {"segments": stats[0], "nodes": stats[1], "tris": stats[2], "nan_alive": stats[3]}
     if sigs is not None:
         st["signatures"] = sigs
     return img, img8, st

@@ -645,7 +645,11 @@ __global__ __launch_bounds__(PT_BLOCK) void material_consts_kernel(DevMaterial* 
     m.ratio_back = m.refraction_index / air_n;
     m.tir_front = asin_pt(m.ratio_back);
     m.tir_back = asin_pt(m.ratio_front);
-    m.spec_zero = m.specular[0] == 0.0f && m.specular[1] == 0.0f && m.specular[2] == 0.0f;
+    // the zero-specular shortcut (shade_hit): a zero specular colour, and a GGX alpha for which the shadow term is
+    // finite on (near-)unit vectors (alpha^2 normal and > 0, alpha <= 4). alpha == 0 (roughness 0) is excluded:
+    // ggx_g1 is 2 / (1 + sqrt(1 + 0 * inf)) = NaN when (v.n)^2 underflows, and the reference keeps that path.
+    m.spec_zero = m.specular[0] == 0.0f && m.specular[1] == 0.0f && m.specular[2] == 0.0f &&
+                  m.rough_alpha >= 0x1p-60f && m.rough_alpha <= 4.0f;
 }
 
 hipError_t launch_material_consts(DevMaterial* mats, int n, float air_n, hipStream_t stream) {
@@ -869,11 +873,13 @@ static PassFnU pass_fn_u(int minw, int feat, int* feat_used, int* minw_used) {
 // pass_kernel_u keeps every material and sphere in LDS: scenes whose tables exceed PT_LDS_TABLES bytes
 // (about 256 materials and 256 spheres) run pass_kernel.
 #define PT_LDS_TABLES (32 * 1024)
-static bool use_unified(bool leaf1, bool stats, int lds_bytes) {
-    return leaf1 && !stats && unified_enabled() && lds_bytes <= PT_LDS_TABLES;
+// pass_kernel_u walks the inline-leaf layout only (walk_box_inline): without it (leaf size > 1, or a leaf whose
+// skip index is not the next record) the launch runs pass_kernel, which follows every node's own skip index
+static bool use_unified(const PassChoice& pc, int lds_bytes) {
+    return pc.leaf1 && pc.il && !pc.stats && unified_enabled() && lds_bytes <= PT_LDS_TABLES;
 }
 
-bool pass_uses_unified(const PassChoice& pc, int lds_bytes) { return use_unified(pc.leaf1, pc.stats, lds_bytes); }
+bool pass_uses_unified(const PassChoice& pc, int lds_bytes) { return use_unified(pc, lds_bytes); }
 
 // The inline-leaf copy of the node array that pass_kernel_u walks (pt_path.h walk_box_inline): record k of
 // `nodes` goes to record np[k] of `out`; a leaf (slot >= 0, one triangle per leaf) takes two records,
@@ -921,7 +927,7 @@ hipError_t launch_inline_leaves(const float4* nodes, const float4* tri_geom, con
 
 hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int first_pass, int batch_log2,
                        int write_u8, int grid, int lds_bytes, hipStream_t stream) {
-    if (use_unified(pc.leaf1, pc.stats, lds_bytes)) {
+    if (use_unified(pc, lds_bytes)) {
         // 64-unit chunks, a 28-lane shading batch, 7 walk steps per round, triangle batches of 6 lanes:
         // measured best with frames in flight (7 steps since the end of round 3: metric
         // +0.4 %, C3 +0.9 %, C4/C5 +0.1-0.3 %, profiles/r03/walk_steps/)
@@ -970,7 +976,7 @@ hipError_t launch_u8(const DevConfig& cfg, const float* image, uint8_t* image256
 // from the instance pass_fn_u actually selects.
 std::string pass_kernel_desc(const PassChoice& pc, int lds_bytes) {
     char buf[160];
-    if (use_unified(pc.leaf1, pc.stats, lds_bytes)) {
+    if (use_unified(pc, lds_bytes)) {
         int fu, wu;
         (void)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, &fu, &wu);
         static const int prof = env_int("PT_UPROF", 0, 0, 1);
@@ -987,7 +993,7 @@ int pass_grid_size(const PassChoice& pc, int lds_bytes) {
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
-    const bool u = use_unified(pc.leaf1, pc.stats, lds_bytes);
+    const bool u = use_unified(pc, lds_bytes);
     int fu, wu;
     const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, &fu, &wu)
                        : (const void*)pass_fn(pc.leaf1, pc.stats, pass_min_waves(false, pc.feat));

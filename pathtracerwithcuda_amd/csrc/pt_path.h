@@ -549,6 +549,13 @@ __device__ __forceinline__ void generate_path(const DevCamera& cam, const DevCon
     ps->d = normalize(image_plane - ap);
 }
 
+// The kill test (path_tracer_kernel.cu:612-616, and :484-487 after a scatter): the reference ends a path
+// iff length(thr) <= energy_exist_threshold, so a NaN throughput (NaN <= x is false) keeps the path going.
+// Tested as !(dot(thr, thr) <= energy_len2), the same unordered outcome (DevConfig::energy_len2).
+__device__ __forceinline__ bool alive_after(v3 thr, const DevConfig& cfg) {
+    return !(dot(thr, thr) <= cfg.energy_len2);
+}
+
 // Closest hit over all spheres then every mesh BVH (path_tracer_kernel.cu:418-454).
 struct Hit {
     float t, t1, t2;
@@ -594,6 +601,13 @@ __device__ __forceinline__ int32_t path_seed(int32_t hseed, int pixel) { return 
 #define PT_FEAT_TEX 2
 #define PT_FEAT_ALL 3
 
+// The zero-specular shortcut's per-lane conditions (shade_hit): thr finite, |d|^2 and |n|^2 <= 1 + 2^-12, and
+// the energy bound non-negative. Comparisons are false for NaN, so a NaN anywhere refuses the shortcut.
+__device__ __forceinline__ bool spec_zero_ok(v3 thr, v3 d, v3 n, const DevConfig& cfg) {
+    const float lim = 1.0f + 0x1p-12f;
+    return dot(thr, thr) < __builtin_inff() && dot(d, d) <= lim && dot(n, n) <= lim && cfg.energy_len2 >= 0.0f;
+}
+
 template <bool STATS, int FEAT = PT_FEAT_ALL>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
                                           PathState* ps, const Hit& h, Counters* ctr, unsigned long long* pc = nullptr);
@@ -638,7 +652,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
                 ps->d = sample_sphere(r1, r2);
                 ps->thr = ps->thr * absorption(sa, dist);
                 if (STATS) ctr->scatter++;
-                return dot(ps->thr, ps->thr) > cfg.energy_len2;  // length(thr) > energy_threshold
+                return alive_after(ps->thr, cfg);
             }
             ps->thr = ps->thr * absorption(sa, min_t);
         }
@@ -717,11 +731,15 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
     float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
     float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
     if (reflect || !transparent) {
-        // A reflection off a material whose specular colour is (0, 0, 0) leaves thr * (spec * shadow) = 0 (or NaN
-        // where thr is infinite), whatever the sampled direction: the kill test (:612-616) ends the path with its
-        // radiance untouched (the reflect branch adds none), so the GGX sample is not computed. Not when the
-        // configured energy bound is negative (or NaN), where a zero throughput would survive the test.
-        if (reflect && M.spec_zero && cfg.energy_len2 >= 0.0f) return false;
+        // A reflection off a material whose specular colour is (0, 0, 0) leaves thr * (spec * shadow) = thr * (+-0)
+        // = +-0 whatever the sampled direction, provided thr and the shadow term are finite: the kill test
+        // (:612-616) then ends the path with its radiance untouched (the reflect branch adds none), so the GGX
+        // sample is not computed. Where thr * (0 * shadow) could be NaN the reference keeps the path, so the
+        // shortcut needs (spec_zero_ok): thr finite; the shadow finite, which DevMaterial::spec_zero guarantees
+        // with alpha in [2^-60, 4] as long as |d|^2 and |n|^2 are <= 1 + 2^-12 (then c2 = (v.n)^2 <= 1 + 2^-8,
+        // so 1 + alpha^2 (1 - c2) / c2 >= 15/16 and the square root in ggx_g1 is finite; alpha^2 > 0 keeps
+        // alpha^2 * inf = inf); and a non-negative energy bound, under which a zero throughput is killed.
+        if (reflect && M.spec_zero && spec_zero_ok(ps->thr, d, normal, cfg)) return false;
         // both branches take sqrtf(r1) and one more square root: computed once for the batch, with the
         // second one's argument chosen per lane (a batch holds lanes of both kinds)
         const float s1 = sqrt_pt(r1);
@@ -761,7 +779,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
         ps->thr = ps->thr * (ratio_oi * ratio_oi);  // ratio = out_n / in_n
     }
     mark(3);
-    return dot(ps->thr, ps->thr) > cfg.energy_len2;  // length(thr) > energy_threshold
+    return alive_after(ps->thr, cfg);
 }
 
 // pixel_256_transform_gamma_corrected_kernel (path_tracer_kernel.cu:627-682) for one pixel.

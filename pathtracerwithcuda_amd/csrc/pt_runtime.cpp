@@ -204,16 +204,33 @@ bool abi_scene_digest(int mesh_num, pt_bvh_node_device** bvh_nodes, pt_triangle*
             if (!hi || n.triangle_indices > hi) hi = n.triangle_indices;
         }
         if (!leaves) continue;
-        const size_t span = (size_t)(hi - lo) + (size_t)leaf_size;
-        if (span <= 2 * leaves * (size_t)leaf_size + 64) {
-            reg.push_back({lo, span * sizeof(int)});
-            for (size_t k = 0; k < span; k++) max_tri = std::max(max_tri, lo[k]);
+        // max_tri comes from the slots themselves; the span between them (bytes that need not be slots when a
+        // caller allocates the arrays separately) only serves as one hashed region
+        for (int i = 0; i < count; i++) {
+            const pt_bvh_node_device& n = nodes[i];
+            if (!n.is_leaf || !n.triangle_indices) continue;
+            for (int k = 0; k < leaf_size; k++) max_tri = std::max(max_tri, n.triangle_indices[k]);
+        }
+        // one region when the slots tile [lo, hi + leaf_size) exactly (the reference's one array per mesh,
+        // bvh.cpp:284-287), so no byte outside a slot is read
+        bool tiled = (size_t)(hi - lo) % (size_t)leaf_size == 0 && (size_t)(hi - lo) / (size_t)leaf_size + 1 == leaves;
+        if (tiled) {
+            std::vector<char> seen(leaves, 0);
+            for (int i = 0; i < count && tiled; i++) {
+                const pt_bvh_node_device& n = nodes[i];
+                if (!n.is_leaf || !n.triangle_indices) continue;
+                const size_t off = (size_t)(n.triangle_indices - lo);
+                if (off % (size_t)leaf_size != 0 || seen[off / (size_t)leaf_size]) tiled = false;
+                else seen[off / (size_t)leaf_size] = 1;
+            }
+        }
+        if (tiled) {
+            reg.push_back({lo, ((size_t)(hi - lo) + (size_t)leaf_size) * sizeof(int)});
         } else {
             for (int i = 0; i < count; i++) {
                 const pt_bvh_node_device& n = nodes[i];
                 if (!n.is_leaf || !n.triangle_indices) continue;
                 reg.push_back({n.triangle_indices, (size_t)leaf_size * sizeof(int)});
-                for (int k = 0; k < leaf_size; k++) max_tri = std::max(max_tri, n.triangle_indices[k]);
             }
         }
     }
@@ -679,7 +696,15 @@ int upload_stage(pt_context* ctx, const SceneStage& st) {
         for (int c = 0; c < 3; c++)
             if (m.absorption[c] != 0.0f || m.reduced_scattering[c] != 0.0f) ctx->scene_feat |= PT_FEAT_MEDIUM;
     }
-    if (st.leaf_size == 1) {
+    // The inline-leaf layout moves a leaf's walk on to the record after its triangle whether its box passes or
+    // not, which is the reference's walk only when every leaf's skip index is the next node (bvh.cpp's preorder
+    // flatten always makes it so; a caller's node array need not). Otherwise pass_kernel walks the plain nodes.
+    bool leaf_skips_next = true;
+    for (int k = 0; k < (int)(st.nodes.size() / 2) && leaf_skips_next; k++)
+        if (__builtin_bit_cast(int, st.nodes[2 * (size_t)k + 1].w) >= 0 &&
+            __builtin_bit_cast(int, st.nodes[2 * (size_t)k].w) != k + 1)
+            leaf_skips_next = false;
+    if (st.leaf_size == 1 && leaf_skips_next) {
         // record k -> np[k]: every leaf with a triangle before k adds its triangle record
         const int R = (int)(st.nodes.size() / 2);
         std::vector<int> np((size_t)R + 1);
@@ -798,6 +823,7 @@ PassChoice pass_choice(const pt_context* ctx, int feat) {
     pc.leaf1 = ctx->scene.leaf_size == 1;
     pc.stats = ctx->instrumented;
     pc.feat = feat;
+    pc.il = ctx->il_nodes != nullptr;
     return pc;
 }
 

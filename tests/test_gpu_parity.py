@@ -213,6 +213,58 @@ def test_material_and_config_variants(gpu, variant):
     assert_bitwise(img8, ref8, f"{variant} 8-bit")
 
 
+def test_nan_throughput_survives_like_the_reference(gpu):
+    """The kill test is length(thr) <= energy_exist_threshold (path_tracer_kernel.cu:612-616): a NaN throughput
+    is NOT killed there, and the path goes on. Walls that multiply the throughput by 1e25 per diffuse bounce
+    overflow it to inf within two bounces; the next wall has a zero channel, so thr * diffuse = inf * 0 = NaN
+    (and a reflection off a zero-specular wall gives inf * (0 * shadow) = NaN, which the zero-specular shortcut
+    must not end). The oracle counts the segments that kept a NaN path alive; the image must be bit-exact."""
+    sc = pt.Scene()
+    hot = sc.add_material(pt.material(((1e25, 1e25, 1e25), (0, 0, 0), (0, 0, 0), False, 0.01, 1.491, 0.0,
+                                       (0, 0, 0), (0, 0, 0))))
+    zero_g = sc.add_material(pt.material(((0.9, 0.0, 0.9), (0, 0, 0), (0, 0, 0), False, 0.01, 1.491, 0.0,
+                                          (0, 0, 0), (0, 0, 0))))
+    sc.add_mesh(pt.cornell_shapes(), [hot, zero_g, hot, zero_g, hot], position=(0.0, -0.8, 1.0), scale=(0.1, 0.1, 0.3))
+    sc.add_mesh([pt.cube_shape()], [sc.add_material("light")], position=(0.0, 3.1, 0.0), scale=(0.85, 0.05, 0.85))
+    sc.add_sphere((-0.9, 0.0, -0.9), 0.8, "iron")
+    sc.add_sphere((1.3, 0.0, -0.4), 0.8, "glass")
+    sc.set_cube_map(pt.procedural_cube_map(16))
+    sc.build()
+    cfg = pt.configuration(max_tracer_depth=8)
+    cam = pt.camera(64, 40, **BENCH_CAM)
+    img, img8, ref, ref8, st = render_both(gpu, sc, cam, cfg, passes=2)
+    assert st["nan_alive"] > 1000, st
+    assert_bitwise(img, ref, "NaN-throughput float")
+    assert_bitwise(img8, ref8, "NaN-throughput 8-bit")
+
+
+def test_leaf_skip_not_next_record(gpu):
+    """A caller's node array whose leaves skip past the next record (the reference's builders never emit one,
+    but path_tracer_kernel takes any array): when such a leaf's box fails, the walk jumps to its own skip index
+    (path_tracer_kernel.cu:145-149), so the inline-leaf layout (which assumes the next record) must not be used.
+    Every third leaf of the knot's tree skips to the end of the mesh; the image must still equal the oracle's."""
+    sc = pt.cornell_scene(pt.torus_knot(40, 12), cube_length=16)
+    v = sc.view
+    nodes = v.bvh_nodes[2]
+    count = nodes[0].next_node_index
+    changed = 0
+    for k in range(1, count):
+        if nodes[k].is_leaf and nodes[k].next_node_index == k + 1 and k % 3 == 0:
+            nodes[k].next_node_index = count
+            changed += 1
+    assert changed > 10
+    cfg = pt.configuration(max_tracer_depth=6)
+    cam = pt.camera(64, 40, **BENCH_CAM)
+    img, img8, ref, ref8, _ = render_both(gpu, sc, cam, cfg, passes=2)
+    if gpu.schedule() == "persistent":
+        assert not gpu.last_kernel().startswith("pass_kernel_u"), gpu.last_kernel()
+    assert_bitwise(img, ref, "leaf skip float")
+    assert_bitwise(img8, ref8, "leaf skip 8-bit")
+    std = pt.cornell_scene(pt.torus_knot(40, 12), cube_length=16)  # kept alive: the view points into it
+    ref_std, _, _ = oracle.render(std.view, cam, cfg, 1, 2)
+    assert not np.array_equal(ref, ref_std)  # the skips changed the walk
+
+
 def _cube_at(x, y, z, s=0.18):
     c = pt.cube_shape()
     return pt.Shape((c.vertices * s + np.array([x, y, z], np.float32)).astype(np.float32), c.normals, c.uvs)
@@ -283,47 +335,58 @@ def c4_workload():
     return bench.Workload("c4")
 
 
-def _subset(w, h, n=3000, seed=0):
-    return np.sort(np.random.default_rng(seed).choice(w * h, n, replace=False)).astype(np.int32)
-
-
-def _render_workload_subset(r, wl, passes=8, npx=20000, seed=0):
-    """One frame of `passes` passes through the batched launch bench.py times, checked on a pixel
-    subset against the oracle (float running sum and the 8-bit output of the last pass). Returns the
-    launch counts by kind so the caller can pin the launch shape."""
+def _render_workload(r, wl, passes=8):
+    """One WHOLE frame of `passes` passes through the batched launch bench.py times, checked on every pixel
+    against the oracle (float running sum and the 8-bit output of the last pass; the oracle renders the
+    metric frame's 8 passes in ~2.5 s on 16 threads). Returns the launch counts by kind so the caller can
+    pin the launch shape, and the oracle's stats."""
     r.upload(wl.scene, wl.cfg)
     r.setup_frame(wl.width, wl.height)
     r.stats_reset()
     r.render(wl.cam, wl.cfg, 1, passes, write_u8=2)
     r.synchronize()
     launches = {k: r.kernel_time_kind(k)[1] for k in (0, 3)}
+    segments = r.stats()["segments"]
     img, img8 = r.download()
-    sel = _subset(wl.width, wl.height, npx, seed)
-    ref, ref8, st = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, passes, pixels=sel)
-    assert_bitwise(img.reshape(-1, 3)[sel], ref, f"{wl.name} subset float")
-    assert_bitwise(img8.reshape(-1, 3)[sel], ref8, f"{wl.name} subset 8-bit")
-    assert st["segments"] > npx * passes
-    return launches, img
+    ref, ref8, st = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, passes)
+    assert_bitwise(img.reshape(-1, 3), ref, f"{wl.name} whole-frame float")
+    assert_bitwise(img8.reshape(-1, 3), ref8, f"{wl.name} whole-frame 8-bit")
+    assert segments == st["segments"], (segments, st["segments"])
+    return launches, st
+
+
+def test_c1_spheres_only_cornell_at_its_size(bench_gpu):
+    """BASELINE config C1 at its own configuration (bench.py --workload c1): the spheres-only Cornell box
+    (no BVH mesh), 512x512, 4 spp, 4 bounces, the 4 passes in one batched launch: all 262,144 pixels against
+    the oracle, bit for bit."""
+    import bench
+    wl = bench.Workload("c1")
+    assert (wl.width, wl.height, wl.spp, wl.depth) == (512, 512, 4, 4)
+    assert wl.scene.view.mesh_num == 0 and wl.scene.view.sphere_num > 0
+    launches, st = _render_workload(bench_gpu, wl, passes=4)
+    assert launches == {0: 1, 3: 1}, launches
+    assert st["segments"] > 512 * 512 * 4
 
 
 def test_metric_frame_at_the_bench_launch_shape(bench_gpu):
     """bench.py's exact step: the metric workload (1920x1080, Cornell + 70k-triangle knot, depth 8), all
     8 passes in ONE persistent launch (batch_log2 = 3) plus one accumulate_kernel launch (its four-pass
-    float4 groups, path_tracer_kernel.cu:644-651 applied pass after pass), then the 8-bit output."""
+    float4 groups, path_tracer_kernel.cu:644-651 applied pass after pass), then the 8-bit output. Every
+    pixel of the frame against the oracle."""
     import bench
     wl = bench.Workload("metric")
-    launches, _ = _render_workload_subset(bench_gpu, wl, passes=8, npx=30000)
+    launches, _ = _render_workload(bench_gpu, wl, passes=8)
     assert launches == {0: 1, 3: 1}, launches
 
 
 def test_c2_diffuse_mesh_frame(bench_gpu):
     """BASELINE config C2 as its own workload (bench.py --workload c2): the Cornell walls and light with
-    the 70k-triangle mesh, diffuse only, no spheres, 1280x720, 8 passes at the bench launch shape.
-    Pixel subset against the oracle."""
+    the 70k-triangle mesh, diffuse only, no spheres, 1280x720, 8 passes at the bench launch shape. Whole
+    frame against the oracle."""
     import bench
     wl = bench.Workload("c2")
     assert (wl.width, wl.height, wl.spp, wl.depth) == (1280, 720, 8, 8) and wl.scene.view.sphere_num == 0
-    launches, _ = _render_workload_subset(bench_gpu, wl, passes=8, npx=20000, seed=2)
+    launches, _ = _render_workload(bench_gpu, wl, passes=8)
     assert launches == {0: 1, 3: 1}, launches
 
 
@@ -331,29 +394,29 @@ def test_c3_microfacet_sky_dof_frame(bench_gpu):
     """BASELINE config C3: six GGX spheres (roughness 0.01..1, a conductor), the skybox and a thin-lens
     camera at 1920x1080, depth 8. 16 passes run as two batched launches of 8: the second batch's
     accumulate adds into the running sum the first left (path_tracer_kernel.cu:644-651, pass_counter > 1).
-    Pixel subset against the oracle."""
+    Whole frame against the oracle."""
     import bench
     wl = bench.Workload("c3")
     assert wl.cam.aperture_radius > 0.0 and wl.scene.view.sphere_num == 6
-    launches, _ = _render_workload_subset(bench_gpu, wl, passes=16, npx=10000)
+    launches, _ = _render_workload(bench_gpu, wl, passes=16)
     assert launches == {0: 2, 3: 2}, launches
 
 
 def test_c4_800k_sss_frame(bench_gpu, c4_workload):
     """BASELINE config C4: the 800k-triangle knot with the DragonGreen subsurface medium at 1920x1080,
-    depth 8, 8 passes in one launch, pixel subset against the oracle."""
+    depth 8, 8 passes in one launch, whole frame against the oracle."""
     assert c4_workload.scene.triangle_count >= 800000
-    launches, _ = _render_workload_subset(bench_gpu, c4_workload, passes=8)
+    launches, _ = _render_workload(bench_gpu, c4_workload, passes=8)
     assert launches == {0: 1, 3: 1}, launches
 
 
 def test_c5_4k_textured_depth12_frame(bench_gpu):
     """BASELINE config C5: three textured knots + a textured cube (diffuse and specular maps) at 3840x2160,
-    depth 12, 8 passes in one launch, pixel subset against the oracle."""
+    depth 12, 8 passes in one launch, whole frame (8.3 M pixels) against the oracle."""
     import bench
     wl = bench.Workload("c5")
     assert wl.depth == 12 and (wl.width, wl.height) == (3840, 2160)
-    launches, _ = _render_workload_subset(bench_gpu, wl, passes=8)
+    launches, _ = _render_workload(bench_gpu, wl, passes=8)
     assert launches == {0: 1, 3: 1}, launches
 
 
