@@ -154,7 +154,8 @@ class Workload:
 
 
 def cpu_baseline(wl: "Workload", threads: int) -> dict:
-    """The reference's CPU fallback semantics (Core/path_tracer_cpu.cpp: MSVC rand, libm), as
+    """The reference's CPU fallback semantics (Core/path_tracer_cpu.cpp: MSVC rand, libm, MSVC's unfused
+    arithmetic), as
     restated by the oracle, on the same frame: one whole frame (all of its passes), so ms/frame is measured,
     not extrapolated."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -162,12 +163,12 @@ def cpu_baseline(wl: "Workload", threads: int) -> dict:
 
     oracle.lib()
     t0 = time.perf_counter()
-    _, _, st = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, wl.spp, rng="msvc", math="libm", threads=threads,
-                             with_u8=True)
+    _, _, st = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, wl.spp, rng="msvc", math="libm", arith="plain",
+                             threads=threads, with_u8=True)
     dt = time.perf_counter() - t0
     return {"value": round(st["segments"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"one whole {wl.width}x{wl.height} {wl.spp}-spp depth-{wl.depth} frame ({st['segments']} ray "
-                      f"segments, {dt:.2f} s), oracle in reference-CPU-fallback mode (MSVC rand, libm), OpenMP",
+                      f"segments, {dt:.2f} s), oracle in reference-CPU-fallback mode (MSVC rand, libm, no FMA), OpenMP",
             "ms_per_frame": round(dt * 1000, 1)}
 
 
@@ -210,6 +211,9 @@ def main() -> int:
     ap.add_argument("--save-image", default="")
     ap.add_argument("--schedule", choices=["persistent", "wavefront"], default=None,
                     help="kernel schedule (default: the library's, PT_MODE)")
+    ap.add_argument("--medium-bound", action="store_true",
+                    help="tolerance mode pt_set_medium_bound: in-medium segments walk with min_t starting at their "
+                         "free-flight distance (not proven bit-exact; DESIGN.md §4.2)")
     ap.add_argument("--workload", choices=["metric", "c1", "c2", "c3", "c4", "c5"], default="metric",
                     help="metric: BASELINE.json's metric configuration (default); c1: its CPU-path plumbing config "
                          "(the line then carries that frame's CPU-path time as cpu_baseline); c2-c5: its other configs")
@@ -278,6 +282,8 @@ def main() -> int:
         q = pt.Renderer(local)
         q.set_schedule(args.schedule)
         q.set_grid_share(grid_share)
+        if args.medium_bound:
+            q.set_medium_bound(True)
         q.upload(scene, cfg)
         rs.append(q)
         frames.append(pt.TiledFrame(q, width, height, dist if world > 1 else None, BAND_ROWS,
@@ -345,6 +351,24 @@ def main() -> int:
         dist.barrier()
     latency = (time.perf_counter() - t1) / max(lat_frames, 1)
     solo_ms, solo_launches = r.kernel_time_kind(kind)
+
+    # N > 1: the tiled frame must be the 1-GPU frame. Outside the timed region, rank 0 renders the same frame
+    # alone on a fresh untiled context over the whole grid and compares it bitwise (float running sum and 8-bit
+    # image) with the frame its tiled context just gathered (the last frame of the latency loop above)
+    matches_1gpu = None
+    if world > 1 and rank == 0:
+        tiled, tiled8 = r.download()
+        solo = pt.Renderer(local)
+        try:
+            if args.medium_bound:
+                solo.set_medium_bound(True)
+            solo.upload(scene, cfg)
+            solo.setup_frame(width, height)
+            solo.render(cam, cfg, 1, spp, write_u8=2)
+            one, one8 = solo.download()
+        finally:
+            solo.close()
+        matches_1gpu = bool(np.array_equal(tiled.view(np.uint32), one.view(np.uint32)) and np.array_equal(tiled8, one8))
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
@@ -429,6 +453,7 @@ def main() -> int:
             "width": width, "height": height, "spp": spp, "max_depth": wl.depth,
             "parallelism": f"tiled{world}" if world > 1 else "single",
             "schedule": schedule,
+            "medium_bound": bool(args.medium_bound),
             "band_rows": BAND_ROWS if world > 1 else None,
             "ms_per_frame": round(ms_per_step, 3),
             "frames_in_flight": inflight,
@@ -465,6 +490,8 @@ def main() -> int:
         },
         "cpu_baseline": None,
     }
+    if world > 1:
+        line["config"]["image_matches_1gpu"] = matches_1gpu
     if world == 1 and not args.no_cpu_baseline and args.workload in ("metric", "c1"):
         threads, why = host_threads(args.cpu_threads)
         line["cpu_baseline"] = cpu_baseline(wl, threads)
@@ -473,6 +500,9 @@ def main() -> int:
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+        if not matches_1gpu:
+            print("[bench] the tiled frame differs from the 1-GPU frame", file=sys.stderr)
+            return 3
     return 0
 
 

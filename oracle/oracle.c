@@ -13,6 +13,9 @@
  *        OR_RNG_MSVC   (1): srand/rand with MSVC CRT semantics (RAND_MAX 0x7fff), seeded as
  *                           path_tracer_cpu.cpp:285,368 — the reference CPU fallback itself.
  *   math OR_MATH_CEPHES / OR_MATH_LIBM (oracle_math.h).
+ *   arithmetic: the reference CUDA build's fused multiply-adds written out at the sites nvcc's default
+ *        contraction gives (oracle_math.h or_fma; the HIP kernel writes the same fmaf), or "plain" (the
+ *        same sites unfused: the MSVC-built CPU fallback, or an nvcc --fmad=false build).
  * Scene input is the reference's own data layout (include/pt_types.h): triangle.mat and
  * bvh_node_device.triangle_indices are dereferenced exactly as the reference does.
  *
@@ -120,8 +123,11 @@ typedef struct {
  * kept the path (reported so a test can show that its scene reaches that case) */
 typedef struct { unsigned long long nodes, tris, nan; } or_counts;
 
-/* path_tracer_kernel.cu:46-52 */
-static or_v3 reflection(or_v3 n, or_v3 in) { return v_sub(in, s_scale(2.0f * v_dot(n, in), n)); }
+/* the product's medium-bounded walk (PT_MEDIUM_BOUND), set per render from bit 9 of math_mode */
+static int or_medium_bound = 0;
+
+/* path_tracer_kernel.cu:46-52: in - (2 dot) n, contracted */
+static or_v3 reflection(or_v3 n, or_v3 in) { return v_fma(n, -(2.0f * v_dot(n, in)), in); }
 
 /* :54-83 */
 static or_v3 refraction(or_v3 n, or_v3 in, float in_n, float out_n) {
@@ -129,24 +135,24 @@ static or_v3 refraction(or_v3 n, or_v3 in, float in_n, float out_n) {
     float ndi = v_dot(n, i);
     float ratio = in_n / out_n;
     float a = ratio * ndi;
-    float b = 1.0f - ratio * ratio * (1.0f - ndi * ndi);
+    float b = or_fma(-(ratio * ratio), or_fma(-ndi, ndi, 1.0f), 1.0f);  /* 1 - r r (1 - ndi ndi) */
     if (b < 0.0f) return v3(0.0f, 0.0f, 0.0f);
-    if (ndi > 0) return v_sub(v_scale(n, a - sqrtf(b)), s_scale(ratio, i));
-    return v_sub(v_scale(n, a + sqrtf(b)), s_scale(ratio, i));
+    float q = ndi > 0 ? a - sqrtf(b) : a + sqrtf(b);                     /* n q - r i, left product fused */
+    return v3(or_fma(n.x, q, -(ratio * i.x)), or_fma(n.y, q, -(ratio * i.y)), or_fma(n.z, q, -(ratio * i.z)));
 }
 
 /* Core/sphere.h:18-55 */
 static int sphere_intersect(const pt_sphere* s, or_v3 o, or_v3 d, or_v3* hp, or_v3* hn, float* ht) {
     or_v3 op = v_sub(f3(s->center), o);
     float b = v_dot(op, d);
-    float delta = b * b - v_dot(op, op) + s->radius * s->radius;
+    float delta = or_fma(s->radius, s->radius, or_fma(b, b, -v_dot(op, op)));  /* (b b - op.op) + r r */
     if (delta < 0) return 0;
     float dr = sqrtf(delta);
     float t1 = b - dr, t2 = b + dr;
     if (t1 < 0 && t2 < 0) return 0;
     if (t1 > 0 && t2 > 0) *ht = fminf(t1, t2);
     else *ht = fmaxf(t1, t2);
-    *hp = v_add(o, v_scale(d, *ht));
+    *hp = v_fma(d, *ht, o);  /* origin + direction t, contracted */
     *hn = v_norm(v_sub(*hp, f3(s->center)));
     return 1;
 }
@@ -184,8 +190,8 @@ static int box_intersect(const pt_bounding_box* b, or_v3 o, or_v3 d, float* hit_
 
 /* path_tracer_kernel.cu:85-161 */
 static int mesh_bvh(const or_scene* sc, int m, or_v3 o, or_v3 d, float* ht, float* ht1, float* ht2, int* htri,
-                    or_counts* cnt) {
-    float min_t = INFINITY, min_t1 = INFINITY, min_t2 = INFINITY;
+                    or_counts* cnt, float bound) {
+    float min_t = bound, min_t1 = INFINITY, min_t2 = INFINITY;  /* bound: INFINITY (the reference) */
     int min_tri = -1, hit = 0;
     float box_t = INFINITY;
     const pt_bvh_node_device* nodes = sc->bvh[m];
@@ -229,15 +235,20 @@ static void frame(or_v3 n, or_v3* vi, or_v3* vj) {
 }
 
 /* :163-192 */
+/* ct n + (cos phi st) vi + (sin phi st) vj (:191, :222): ((ct n + c vi) + s vj), each product fused in turn */
+static or_v3 hemi_combine(or_v3 n, float ct, float c, or_v3 vi, float s, or_v3 vj) {
+    return v_fma(vj, s, v_fma(n, ct, v_scale(vi, c)));
+}
+
 static or_v3 hemisphere_cosine(int mm, or_v3 n, float r1, float r2) {
     float ct = sqrtf(r1);
-    float st = sqrtf(1.0f - ct * ct);
+    float st = sqrtf(or_fma(-ct, ct, 1.0f));
     float phi = r2 * OR_TWO_PI;
     or_v3 vi, vj;
     frame(n, &vi, &vj);
     float sp, cp;
     m_sincos(mm, phi, &sp, &cp);
-    return v_add(v_add(s_scale(ct, n), s_scale(cp * st, vi)), s_scale(sp * st, vj));
+    return hemi_combine(n, ct, cp * st, vi, sp * st, vj);
 }
 
 /* :194-223 */
@@ -250,13 +261,13 @@ static or_v3 hemisphere_ggx(int mm, or_v3 n, float rough, float r1, float r2) {
     frame(n, &vi, &vj);
     float sp, cp;
     m_sincos(mm, phi, &sp, &cp);
-    return v_add(v_add(s_scale(ct, n), s_scale(cp * st, vi)), s_scale(sp * st, vj));
+    return hemi_combine(n, ct, cp * st, vi, sp * st, vj);
 }
 
 /* :225-236 */
 static or_v3 on_sphere(int mm, float r1, float r2) {
-    float ct = r1 * 2.0f - 1.0f;
-    float st = sqrtf(1.0f - ct * ct);
+    float ct = or_fma(r1, 2.0f, -1.0f);
+    float st = sqrtf(or_fma(-ct, ct, 1.0f));
     float phi = r2 * OR_TWO_PI;
     float sp, cp;
     m_sincos(mm, phi, &sp, &cp);
@@ -280,8 +291,8 @@ static float ggx_masking(float rough, or_v3 macro, or_v3 micro, or_v3 dir) {
     if (positive == 0.0f) return 0.0f;
     float r2 = rough * rough;
     float c2 = vdn * vdn;
-    float t2 = (1.0f - c2) / c2;
-    return 2.0f / (1.0f + sqrtf(1.0f + r2 * t2));
+    float t2 = or_fma(-vdn, vdn, 1.0f) / c2;
+    return 2.0f / (1.0f + sqrtf(or_fma(r2, t2, 1.0f)));
 }
 
 /* Core/fresnel.h:11-49 */
@@ -290,19 +301,20 @@ static float fresnel_dielectrics(int mm, or_v3 n, or_v3 in, float in_n, float ou
     float cout = v_dot(s_scale(-1.0f, n), refr);
     if (in_n > out_n && m_acos(mm, cin) >= m_asin(mm, out_n / in_n)) return 1.0f;
     if (v_len(refr) <= 0.000005f || cout < 0) return 1.0f;
-    float s = (in_n * cin - out_n * cout) / (in_n * cin + out_n * cout);
-    float p = (in_n * cout - out_n * cin) / (in_n * cout + out_n * cin);
-    return (s * s + p * p) / 2.0f;
+    float s = or_fma(in_n, cin, -(out_n * cout)) / or_fma(in_n, cin, out_n * cout);
+    float p = or_fma(in_n, cout, -(out_n * cin)) / or_fma(in_n, cout, out_n * cin);
+    return or_fma(s, s, p * p) / 2.0f;  /* pow(s, 2) + pow(p, 2): x * x, the left one fused */
 }
 
 /* Core/fresnel.h:51-76 */
 static float fresnel_conductors(or_v3 n, or_v3 in, float eta, float k) {
     float cin = v_dot(n, v_scale(in, -1.0f));
-    float nk = eta * eta + k * k;
+    float nk = or_fma(eta, eta, k * k);
     float c2 = cin * cin;
-    float tnc = 2 * eta * cin;
-    float rs = (nk * c2 - tnc + 1.0f) / (nk * c2 + tnc + 1.0f);
-    float rp = (nk - tnc + c2) / (nk + tnc + c2);
+    float tn = 2 * eta;
+    float tnc = tn * cin;
+    float rs = (or_fma(nk, c2, -tnc) + 1.0f) / (or_fma(nk, c2, tnc) + 1.0f);
+    float rp = or_fma(cin, cin, or_fma(-tn, cin, nk)) / or_fma(cin, cin, or_fma(tn, cin, nk));
     return (rs + rp) / 2.0f;
 }
 
@@ -361,7 +373,7 @@ static or_v3 background(const or_scene* sc, or_v3 d) {
     if (c->use_sky) {
         float t = (v_dot(d, v3(-0.41f, 0.41f, -0.82f)) + 1.0f) / 2.0f;
         or_v3 a = v3(0.15f, 0.3f, 0.5f), b = v3(1.0f, 1.0f, 1.0f);
-        return v_scale(v_add(s_scale(1.0f - t, a), s_scale(t, b)), 1.0f);
+        return v_scale(v_fma(a, 1.0f - t, s_scale(t, b)), 1.0f);  /* ((1 - t) a + t b) * 1 */
     }
     return v3(0.0f, 0.0f, 0.0f);
 }
@@ -398,7 +410,7 @@ static void generate(const or_scene* sc, const pt_render_camera* cam, int rng_ki
 
     float rx = cam->resolution.x, ry = cam->resolution.y;
     int image_y = (int)((float)pixel / rx);
-    int image_x = (int)((float)pixel - ((float)image_y * rx));
+    int image_x = (int)or_fma(-(float)image_y, rx, (float)pixel);
     int32_t hs = or_hash(seed);
     or_rng rng = rng_seed(rng_kind, mulw(mulw(hs, hs), or_hash(pixel)));
     float jx = 0.0f, jy = 0.0f;
@@ -409,10 +421,10 @@ static void generate(const or_scene* sc, const pt_render_camera* cam, int rng_ki
     or_v3 vt = v_norm(v_cross(hz, view));
     or_v3 xa = v_scale(hz, distance * m_tan(mm, cam->fov.x * 0.5f * (OR_PI / 180.0f)));
     or_v3 ya = v_scale(vt, distance * m_tan(mm, -cam->fov.y * 0.5f * (OR_PI / 180.0f)));
-    float nx = (((float)image_x + jx) / (rx - 1.0f)) * 2.0f - 1.0f;
-    float ny = (((float)image_y + jy) / (ry - 1.0f)) * 2.0f - 1.0f;
-    or_v3 canvas = v_add(v_add(v_add(eye, view), s_scale(nx, xa)), s_scale(ny, ya));
-    or_v3 image_plane = v_add(eye, v_scale(v_norm(v_sub(canvas, eye)), cam->focal_distance));
+    float nx = or_fma(((float)image_x + jx) / (rx - 1.0f), 2.0f, -1.0f);
+    float ny = or_fma(((float)image_y + jy) / (ry - 1.0f), 2.0f, -1.0f);
+    or_v3 canvas = v_fma(ya, ny, v_fma(xa, nx, v_add(eye, view)));
+    or_v3 image_plane = v_fma(v_norm(v_sub(canvas, eye)), cam->focal_distance, eye);
     or_v3 ap;
     if (cam->aperture_radius > 0.00001f) {
         float r1 = draw_aperture(&rng), r2 = draw_aperture(&rng);
@@ -420,7 +432,7 @@ static void generate(const or_scene* sc, const pt_render_camera* cam, int rng_ki
         float dist = cam->aperture_radius * sqrtf(r2);
         float sa, ca;
         m_sincos(mm, angle, &sa, &ca);
-        ap = v_add(v_add(eye, s_scale(ca * dist, hz)), s_scale(sa * dist, vt));
+        ap = v_fma(vt, sa * dist, v_fma(hz, ca * dist, eye));
     } else {
         ap = eye;
     }
@@ -451,10 +463,23 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
             min_t = ht; min_point = hp; min_normal = hn; min_sphere = i; type = 1;
         }
     }
+    /* The medium-bounded walk (PT_MEDIUM_BOUND, a tolerance mode of the product, not the reference): a
+     * segment inside a scattering medium draws its free-flight distance first (:463-464; intersection draws
+     * nothing), and a hit beyond it cannot matter, so each mesh walk starts with min_t = dist (1 + 2^-10)
+     * instead of infinity (mesh_bound below). */
+    float bound = INFINITY;
+    if (or_medium_bound) {
+        pt_scattering c0 = st->sca[k];
+        if (c0.reduced_scattering_coefficient.x > 0.0f || v_len(f3(c0.absorption_coefficient)) > cfg->sss_threshold) {
+            or_rng r0 = rng;
+            float dist0 = -m_log(mm, draw01(&r0)) / c0.reduced_scattering_coefficient.x;
+            if (dist0 >= 0.0f && dist0 < INFINITY) bound = dist0 + dist0 * 0x1p-10f;
+        }
+    }
     for (int m = 0; m < sc->mesh_num; m++) {
-        if (mesh_bvh(sc, m, o, d, &ht, &ht1, &ht2, &htri, cnt) && ht < min_t && ht > 0.0f) {
+        if (mesh_bvh(sc, m, o, d, &ht, &ht1, &ht2, &htri, cnt, bound) && ht < min_t && ht > 0.0f) {
             min_t = ht; min_t1 = ht1; min_t2 = ht2;
-            min_point = v_add(o, v_scale(d, ht));
+            min_point = v_fma(d, ht, o);
             min_tri = htri; type = 2;
         }
     }
@@ -466,7 +491,7 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
         if (dist < min_t) {
             sig_add(st, k, 1);  /* scatter inside the medium */
             float r1 = draw01(&rng), r2 = draw01(&rng);
-            st->rays[k].origin = pf3(v_add(o, v_scale(d, dist)));
+            st->rays[k].origin = pf3(v_fma(d, dist, o));
             st->rays[k].direction = pf3(on_sphere(mm, r1, r2));
             st->thr[k] = v_mul(st->thr[k], absorption_through(mm, cs.absorption_coefficient, dist));
             float len = v_len(st->thr[k]);
@@ -486,7 +511,7 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
             sig_add(st, k, 6 + face * 8);
         }
         or_v3 bg = background(sc, d);
-        st->rad[k] = v_add(st->rad[k], v_mul(st->thr[k], bg));
+        st->rad[k] = v_fmav(st->thr[k], bg, st->rad[k]);
         st->alive[ai] = -1;
         return;
     }
@@ -498,12 +523,11 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
         const pt_triangle* tr = &sc->tris[min_tri];
         mat = *tr->mat;
         float w = 1.0f - min_t1 - min_t2;
-        min_normal = v_add(v_add(v_scale(f3(tr->normal0), w), v_scale(f3(tr->normal1), min_t1)),
-                           v_scale(f3(tr->normal2), min_t2));
+        min_normal = v_fma(f3(tr->normal2), min_t2, v_fma(f3(tr->normal0), w, v_scale(f3(tr->normal1), min_t1)));
         float u = 0.0f, v = 0.0f;
         if (mat.diffuse_texture_id != -1 || mat.specular_texture_id != -1) {
-            u = (tr->uv0.x * w + tr->uv1.x * min_t1) + tr->uv2.x * min_t2;
-            v = (tr->uv0.y * w + tr->uv1.y * min_t1) + tr->uv2.y * min_t2;
+            u = or_fma(tr->uv2.x, min_t2, or_fma(tr->uv0.x, w, tr->uv1.x * min_t1));
+            v = or_fma(tr->uv2.y, min_t2, or_fma(tr->uv0.y, w, tr->uv1.y * min_t1));
         }
         float au = u - floorf(u), av = v - floorf(v);
         if (mat.diffuse_texture_id != -1) {
@@ -555,7 +579,7 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
         float ratio = out_n / in_n;  /* :595 __powf(ratio, 2.0f): ratio * ratio, except under the CUDA model */
         st->thr[k] = v_scale(st->thr[k], OR_CK(mm) ? m_pow(mm, ratio, 2.0f) : ratio * ratio);
     } else {
-        st->rad[k] = v_add(st->rad[k], v_mul(st->thr[k], f3(mat.emission_color)));
+        st->rad[k] = v_fmav(st->thr[k], f3(mat.emission_color), st->rad[k]);
         st->thr[k] = v_mul(st->thr[k], f3(mat.diffuse_color));
         float r1 = draw01(&rng), r2 = draw01(&rng);
         st->rays[k].origin = pf3(v_add(min_point, bias));
@@ -598,6 +622,10 @@ int or_render_sig(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangl
                   const pt_configuration* cfg, const pt_render_camera* cam, int first_pass, int pass_count,
                   const int* pixel_list, int n, float* image, unsigned char* image256, int rng_kind, int math_mode,
                   int threads, unsigned long long* stats, unsigned long long* sigs) {
+    /* bit 8 of math_mode: plain arithmetic (the contraction sites evaluated unfused, oracle_math.h or_fma) */
+    or_fma_on = !((math_mode >> 8) & 1);
+    or_medium_bound = (math_mode >> 9) & 1;  /* bit 9: the medium-bounded walk (tolerance mode) */
+    math_mode &= 0xff;
     or_scene sc = {mesh_num, bvh_nodes, triangles, sphere_num, spheres, cube, textures, cfg, math_mode};
     or_state st;
     st.sig = NULL;

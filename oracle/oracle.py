@@ -20,6 +20,9 @@ VARIANTS = {"": LIB, "fma": os.path.join(HERE, "lib", "liboracle_fma.so")}
 RNG = {"thrust": 0, "msvc": 1}
 # "cuda" / "cuda_site": the model of the reference's hardware intrinsics (oracle_math.h), calibration only
 MATH = {"cephes": 0, "libm": 1, "cuda": 2, "cuda_site": 3}
+# "fma": the reference CUDA build's contraction sites as fused multiply-adds (what the HIP kernel computes);
+# "plain": the same sites unfused (the MSVC-built CPU fallback; an nvcc --fmad=false build)
+ARITH = {"fma": 0, "plain": 256}
 
 _libs = {}
 
@@ -59,13 +62,15 @@ def lib(variant: str = "") -> C.CDLL:
 def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.ndarray | None = None,
            rng: str = "thrust", math: str = "cephes", threads: int = 0, with_u8: bool = True,
            image: np.ndarray | None = None, image256: np.ndarray | None = None, variant: str = "",
-           signatures: bool = False):
+           signatures: bool = False, arith: str = "fma", medium_bound: bool = False):
     """Run passes first_pass..first_pass+pass_count-1 over all pixels (or the given pixel indices).
 
     `image` / `image256` (optional, float32 / uint8, n*3 contiguous) are the caller's running sum and
     8-bit buffers, updated in place with the reference's pass_counter semantics (a pass > 1 adds
     into the running sum): the CPU twin's view of Core/path_tracer.cpp:71-91.
-    `variant` "fma" runs the FMA-contracting build (calibration only). `signatures` adds
+    `variant` "fma" runs the build compiled with -ffp-contract=fast (calibration only); `arith` "plain"
+    evaluates the contraction sites unfused (the reference CPU fallback's arithmetic). `medium_bound`:
+    the product's tolerance-mode walk (PT_MEDIUM_BOUND: in-medium segments prune beyond their free flight). `signatures` adds
     stats["signatures"]: uint64 [pass_count, n], a hash of each path's decisions (hit primitive and
     branch per segment): equal signatures = same path topology.
     Returns (image float32 [n,3], image256 uint8 [n,3] or None, stats dict)."""
@@ -92,7 +97,7 @@ def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.
                      view.sphere_num, C.cast(view.spheres, C.c_void_p), C.cast(view.sky_cube_map, C.c_void_p),
                      C.cast(view.mesh_textures, C.c_void_p), C.addressof(cfg), C.addressof(cam), first_pass,
                      pass_count, plist.ctypes.data if plist is not None else None, n, img.ctypes.data,
-                     img8.ctypes.data if img8 is not None else None, RNG[rng], MATH[math], threads, stats,
+                     img8.ctypes.data if img8 is not None else None, RNG[rng], MATH[math] | ARITH[arith] | (512 if medium_bound else 0), threads, stats,
                      sigs.ctypes.data if sigs is not None else None)
     if rc != 0:
         raise MemoryError("oracle allocation failed")

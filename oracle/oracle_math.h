@@ -20,6 +20,16 @@
 
 typedef struct { float x, y, z; } or_v3;
 
+/* Contraction (DESIGN.md §5 "FMA contraction"). The reference's CUDA build contracts a*b+c into fused
+ * multiply-adds (nvcc -fmad=true by default; gpu_path_tracer.vcxproj sets no --fmad=false): a product that is
+ * an operand of an addition or subtraction in the same straight-line code is fused into it, the left product
+ * where both operands are products, additions never reassociated. or_fma() writes out those sites; the rest
+ * of this file is compiled with -ffp-contract=off. or_fma_on = 0 ("plain") evaluates the same sites unfused
+ * (a*b rounded, then + c): the reference CPU fallback (MSVC /fp:precise on SSE2, no FMA) and an nvcc
+ * --fmad=false build. Set once per render, before the parallel loops (oracle.c or_render_sig). */
+static int or_fma_on = 1;
+static inline float or_fma(float a, float b, float c) { return or_fma_on ? fmaf(a, b, c) : a * b + c; }
+
 static inline or_v3 v3(float x, float y, float z) { or_v3 r; r.x = x; r.y = y; r.z = z; return r; }
 static inline or_v3 v_add(or_v3 a, or_v3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 static inline or_v3 v_sub(or_v3 a, or_v3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -27,9 +37,13 @@ static inline or_v3 v_mul(or_v3 a, or_v3 b) { return v3(a.x * b.x, a.y * b.y, a.
 static inline or_v3 v_scale(or_v3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }   /* float3 * float */
 static inline or_v3 s_scale(float s, or_v3 a) { return v3(s * a.x, s * a.y, s * a.z); }   /* float * float3 */
 static inline or_v3 v_divs(or_v3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
-static inline float v_dot(or_v3 a, or_v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }        /* :1389 */
+/* a * s + c and a * b + c per component (the product fused into the addition that consumes it) */
+static inline or_v3 v_fma(or_v3 a, float s, or_v3 c) { return v3(or_fma(a.x, s, c.x), or_fma(a.y, s, c.y), or_fma(a.z, s, c.z)); }
+static inline or_v3 v_fmav(or_v3 a, or_v3 b, or_v3 c) { return v3(or_fma(a.x, b.x, c.x), or_fma(a.y, b.y, c.y), or_fma(a.z, b.z, c.z)); }
+/* :1389 (a.x*b.x + a.y*b.y) + a.z*b.z, contracted */
+static inline float v_dot(or_v3 a, or_v3 b) { return or_fma(a.z, b.z, or_fma(a.x, b.x, a.y * b.y)); }
 static inline or_v3 v_cross(or_v3 a, or_v3 b) {                                                    /* :1581 */
-    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+    return v3(or_fma(a.y, b.z, -(a.z * b.y)), or_fma(a.z, b.x, -(a.x * b.z)), or_fma(a.x, b.y, -(a.y * b.x)));
 }
 static inline float v_len(or_v3 a) { return sqrtf(v_dot(a, a)); }                                   /* :1438 */
 /* :1458 — host rsqrtf of cuda_math.hpp:33-36 is 1.0f / sqrtf(x); the device's rsqrtf under the CUDA
@@ -41,7 +55,7 @@ static inline or_v3 v_norm(or_v3 a) {
     float inv = or_ck_mode ? ck_rsqrt(d) : 1.0f / sqrtf(d);
     return v_scale(a, inv);
 }
-static inline or_v3 v_lerp(or_v3 a, or_v3 b, float t) { return v_add(a, s_scale(t, v_sub(b, a))); } /* :1260 */
+static inline or_v3 v_lerp(or_v3 a, or_v3 b, float t) { return v_fma(v_sub(b, a), t, a); }          /* :1260 */
 static inline float or_clamp(float f, float a, float b) { return fmaxf(a, fminf(f, b)); }           /* :1290 */
 
 static inline uint32_t or_f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }

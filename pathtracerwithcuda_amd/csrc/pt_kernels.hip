@@ -219,10 +219,11 @@ __device__ __forceinline__ bool start_mesh_next(const int4* lds_next, int& mesh,
     return e.x != e.y;
 }
 
-// A mesh walk's start state over node range r (the walk's local min_t starts at infinity).
-__device__ __forceinline__ void walk_start(MeshWalk& w, int2 r) {
+// A mesh walk's start state over node range r (the walk's local min_t starts at infinity; at the segment's
+// medium bound in the medium-bounded mode, pt_path.h medium_bound).
+__device__ __forceinline__ void walk_start(MeshWalk& w, int2 r, float t0 = __builtin_inff()) {
     w.pos = r.x; w.end = r.y;
-    w.t = __builtin_inff(); w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
+    w.t = t0; w.t1 = 0.0f; w.t2 = 0.0f; w.tri = -1;
 }
 
 // ---- root boxes at segment start (at most PT_ROOT_MESHES meshes) ----------------------------------
@@ -244,7 +245,7 @@ __device__ __forceinline__ int2 root_walk_range(const int2* lds_mesh, const floa
 // the walk state is set once from them, so the compiler merges no walk fields between the two.
 __device__ __forceinline__ int begin_segment(const DevScene& sc, bool roots, const int2* lds_mesh,
                                              const float4* lds_root, const PathState& ps, v3& inv, Hit& h,
-                                             MeshWalk& w, int& mesh) {
+                                             MeshWalk& w, int& mesh, float t0 = __builtin_inff()) {
     h.t = __builtin_inff(); h.t1 = __builtin_inff(); h.t2 = __builtin_inff();
     h.type = 0; h.prim = -1;
     for (int i = 0; i < sc.sphere_num; i++) {
@@ -264,7 +265,7 @@ __device__ __forceinline__ int begin_segment(const DevScene& sc, bool roots, con
             const int2 r = lds_mesh[i];
             if (r.x == r.y) continue;
             float entry;
-            if (box_hit(lds_root[2 * i], lds_root[2 * i + 1], ps.o, inv, &entry) && entry <= __builtin_inff())
+            if (box_hit(lds_root[2 * i], lds_root[2 * i + 1], ps.o, inv, &entry) && entry <= t0)
                 todo |= 1u << i;
         }
         any = todo != 0u;
@@ -273,7 +274,7 @@ __device__ __forceinline__ int begin_segment(const DevScene& sc, bool roots, con
         range = root_walk_range(lds_mesh, lds_root, m);
     }
     mesh = first;
-    walk_start(w, range);
+    walk_start(w, range, t0);
     return any ? LANE_WALK : LANE_READY;
 }
 // The next mesh of a root-masked segment (mesh_done) and its walk range: false when none is left.
@@ -364,6 +365,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     int32_t pseed = 0;
     int depth = 0;
     int mode = LANE_WANT;
+    float wbound = __builtin_inff();  // every mesh walk's starting min_t (medium-bounded mode only)
     unsigned long long segments = 0;  // wave-uniform: lanes shaded (ray segments traced)
     Counters none = {0u, 0u, 0u, 0u, 0u, 0u};
     const unsigned int units = (unsigned int)P0->til.unit_count << batch_log2;
@@ -434,7 +436,12 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             }
         }
         if (mode == LANE_NEW) {
-            mode = begin_segment(sc, roots, lds_mesh, lds_root, ps, inv, h, w, mesh);
+            if ((FEAT & PT_FEAT_MEDIUM) && cfg.medium_bound) {
+                wbound = medium_bound(sc, cfg, ps.medium, depth, pseed);
+                mode = begin_segment(sc, roots, lds_mesh, lds_root, ps, inv, h, w, mesh, wbound);
+            } else {
+                mode = begin_segment(sc, roots, lds_mesh, lds_root, ps, inv, h, w, mesh);
+            }
         }
         if (!__any(mode != LANE_DONE)) break;
         if (PROF) { const unsigned long long t = __builtin_readcyclecounter(); prof[8] += t - tc; tc = t; }
@@ -488,7 +495,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             }
             // the walk state is reset whether or not a mesh is left (a READY lane does not read it), so
             // the branches above only produce a range and the compiler merges no walk fields
-            walk_start(w, range);
+            walk_start(w, range, (FEAT & PT_FEAT_MEDIUM) ? wbound : __builtin_inff());
             mode = more ? LANE_WALK : LANE_READY;
         };
         // the parked triangle's geometry, loaded at the park; scoped to the walk loop, which no lane leaves

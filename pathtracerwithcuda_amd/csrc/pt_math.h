@@ -8,10 +8,15 @@
 //
 // Determinism contract: this file is compiled with -ffp-contract=off
 // and without fast-math, so every +,-,*,/ and sqrtf is a single IEEE-754 correctly rounded
-// operation on gfx950 exactly as on x86-64 SSE. The transcendentals below use only those
-// operations (Cephes single-precision algorithms with fixed coefficients), so a host restatement
-// of the same algorithm reproduces the GPU bit-for-bit. normalize() uses 1/sqrtf (two correctly
-// rounded ops) in place of the reference's rsqrtf approximation.
+// operation on gfx950 exactly as on x86-64, and every fused multiply-add is written out as fmaf
+// where the reference's CUDA build contracts one (nvcc's default -fmad=true; DESIGN.md §5 "FMA
+// contraction"): a product that is an operand of an addition or subtraction in the same straight-
+// line code is fused into it, the left product where both operands are products, and additions are
+// never reassociated. The oracle writes the same fmaf at the same sites. The transcendentals below
+// are Cephes single-precision algorithms with fixed coefficients, kept unfused (they stand in for
+// the CUDA intrinsics, which are not source the compiler contracts), so a host restatement of the
+// same algorithm reproduces the GPU bit-for-bit. normalize() uses 1/sqrtf (two correctly rounded
+// ops) in place of the reference's rsqrtf approximation.
 #pragma once
 
 #include <stdint.h>
@@ -48,11 +53,17 @@ PT_HD v3 operator/(float s, v3 a) { return mk3(s / a.x, s / a.y, s / a.z); }
 PT_HD v2 operator+(v2 a, v2 b) { return mk2(a.x + b.x, a.y + b.y); }
 PT_HD v2 operator*(v2 a, float s) { return mk2(a.x * s, a.y * s); }
 
-// cuda_math.hpp:1389
-PT_HD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-// cuda_math.hpp:1581
+// a * s + c per component (a float3 * float product fused into the addition that consumes it)
+PT_HD v3 fma3(v3 a, float s, v3 c) { return mk3(fmaf(a.x, s, c.x), fmaf(a.y, s, c.y), fmaf(a.z, s, c.z)); }
+// a * b + c per component
+PT_HD v3 fma3v(v3 a, v3 b, v3 c) { return mk3(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z)); }
+
+// cuda_math.hpp:1389, (a.x*b.x + a.y*b.y) + a.z*b.z contracted: the left product of the inner sum is fused
+// with the right one, then the last product with the sum
+PT_HD float dot(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.x, b.x, a.y * b.y)); }
+// cuda_math.hpp:1581, each a*b - c*d contracted as fmaf(a, b, -(c*d))
 PT_HD v3 cross(v3 a, v3 b) {
-    return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+    return mk3(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
 }
 #if defined(__HIPCC__)
 // 1.0f / x correctly rounded (the IEEE division of the reference and the oracle), from v_rcp_f32
@@ -103,8 +114,8 @@ PT_HD v3 normalize(v3 v) {
 #endif
     return v * inv_len;
 }
-// cuda_math.hpp:1260
-PT_HD v3 lerp(v3 a, v3 b, float t) { return a + t * (b - a); }
+// cuda_math.hpp:1260, a + t*(b - a) contracted
+PT_HD v3 lerp(v3 a, v3 b, float t) { return fma3(b - a, t, a); }
 // cuda_math.hpp:1290,1300 (fmaxf(a, fminf(f, b)))
 PT_HD float clampf(float f, float a, float b) { return fmaxf(a, fminf(f, b)); }
 PT_HD v3 clamp3(v3 v, float a, float b) { return mk3(clampf(v.x, a, b), clampf(v.y, a, b), clampf(v.z, a, b)); }

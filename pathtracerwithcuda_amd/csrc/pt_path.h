@@ -1,7 +1,9 @@
 // pt_path.h — per-ray device functions of the radiance loop.
 //
 // Each function restates one reference function (file:line given); the operation order of
-// every float expression follows the reference source so that, with contraction off, the
+// every float expression follows the reference source, and the fused multiply-adds of the
+// reference's CUDA build (nvcc -fmad=true) are written out as fmaf at the sites its contraction
+// rule gives (pt_math.h header), the rest compiled with contraction off, so the
 // result is reproducible on the host (oracle/) bit-for-bit.
 #pragma once
 
@@ -53,9 +55,10 @@ __device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int byte_offse
     return f;
 }
 
-// path_tracer_kernel.cu:46-52
+// path_tracer_kernel.cu:46-52: in - (2 dot) n, the product fused into the subtraction
 __device__ __forceinline__ v3 reflection(v3 n, v3 in) {
-    return in - 2.0f * dot(n, in) * n;
+    const float s = -(2.0f * dot(n, in));
+    return fma3(n, s, in);
 }
 
 // path_tracer_kernel.cu:54-83; ratio = in_n / out_n (a per-material constant, DevMaterial::ratio_front /
@@ -64,10 +67,12 @@ __device__ __forceinline__ v3 refraction(v3 n, v3 in, float ratio) {
     v3 i = in * -1.0f;
     float ndi = dot(n, i);
     float a = ratio * ndi;
-    float b = 1.0f - ratio * ratio * (1.0f - ndi * ndi);
+    // 1 - (r r)(1 - ndi ndi), both subtractions of a product contracted
+    float b = fmaf(-(ratio * ratio), fmaf(-ndi, ndi, 1.0f), 1.0f);
     if (b < 0.0f) return mk3(0.0f, 0.0f, 0.0f);
-    if (ndi > 0) return n * (a - sqrt_pt(b)) - ratio * i;
-    return n * (a + sqrt_pt(b)) - ratio * i;
+    // n (a -+ sqrt b) - r i: the left product fused
+    const float q = ndi > 0 ? a - sqrt_pt(b) : a + sqrt_pt(b);
+    return mk3(fmaf(n.x, q, -(ratio * i.x)), fmaf(n.y, q, -(ratio * i.y)), fmaf(n.z, q, -(ratio * i.z)));
 }
 
 // Orthonormal frame of sample_on_hemisphere_* (path_tracer_kernel.cu:175-189). The reference
@@ -82,6 +87,12 @@ __device__ __forceinline__ void tangent_frame(v3 n, v3* vi, v3* vj) {
     *vj = cross(n, *vi);
 }
 
+// cos_theta n + (cos phi sin_theta) vi + (sin phi sin_theta) vj (path_tracer_kernel.cu:191,222), contracted:
+// ((ct n + c vi) + s vj) -> fmaf(s, vj, fmaf(ct, n, c vi))
+__device__ __forceinline__ v3 hemisphere_combine(v3 n, float cos_theta, float c, v3 vi, float s, v3 vj) {
+    return fma3(vj, s, fma3(n, cos_theta, vi * c));
+}
+
 // The common tail of sample_on_hemisphere_cosine_weight / _ggx_weight (path_tracer_kernel.cu:174-191):
 // the tangent frame of n and the direction at (theta, phi = 2 pi r2).
 __device__ __forceinline__ v3 hemisphere_dir(v3 n, float cos_theta, float sin_theta, float r2) {
@@ -90,19 +101,19 @@ __device__ __forceinline__ v3 hemisphere_dir(v3 n, float cos_theta, float sin_th
     tangent_frame(n, &vi, &vj);
     float sp, cp;
     sincos_pt(phi, &sp, &cp);
-    return cos_theta * n + cp * sin_theta * vi + sp * sin_theta * vj;
+    return hemisphere_combine(n, cos_theta, cp * sin_theta, vi, sp * sin_theta, vj);
 }
 
 // path_tracer_kernel.cu:163-192
 __device__ __forceinline__ v3 sample_cosine(v3 n, float r1, float r2) {
     float cos_theta = sqrt_pt(r1);
-    float sin_theta = sqrt_pt(1.0f - cos_theta * cos_theta);
+    float sin_theta = sqrt_pt(fmaf(-cos_theta, cos_theta, 1.0f));
     float phi = r2 * kTWO_PI;
     v3 vi, vj;
     tangent_frame(n, &vi, &vj);
     float sp, cp;
     sincos_pt(phi, &sp, &cp);
-    return cos_theta * n + cp * sin_theta * vi + sp * sin_theta * vj;
+    return hemisphere_combine(n, cos_theta, cp * sin_theta, vi, sp * sin_theta, vj);
 }
 
 // path_tracer_kernel.cu:194-223
@@ -115,13 +126,13 @@ __device__ __forceinline__ v3 sample_ggx(v3 n, float roughness, float r1, float 
     tangent_frame(n, &vi, &vj);
     float sp, cp;
     sincos_pt(phi, &sp, &cp);
-    return cos_theta * n + cp * sin_theta * vi + sp * sin_theta * vj;
+    return hemisphere_combine(n, cos_theta, cp * sin_theta, vi, sp * sin_theta, vj);
 }
 
 // path_tracer_kernel.cu:225-236
 __device__ __forceinline__ v3 sample_sphere(float r1, float r2) {
-    float cos_theta = r1 * 2.0f - 1.0f;
-    float sin_theta = sqrt_pt(1.0f - cos_theta * cos_theta);
+    float cos_theta = fmaf(r1, 2.0f, -1.0f);
+    float sin_theta = sqrt_pt(fmaf(-cos_theta, cos_theta, 1.0f));
     float phi = r2 * kTWO_PI;
     float sp, cp;
     sincos_pt(phi, &sp, &cp);
@@ -147,8 +158,8 @@ __device__ __forceinline__ float ggx_g1(float roughness, v3 macro, v3 micro, v3 
     if (!positive) return 0.0f;
     float r2 = roughness * roughness;
     float c2 = vdn * vdn;
-    float t2 = (1.0f - c2) / c2;
-    return 2.0f / (1.0f + sqrt_pt(1.0f + r2 * t2));
+    float t2 = fmaf(-vdn, vdn, 1.0f) / c2;  // (1 - c2) / c2, the product fused into the subtraction
+    return 2.0f / (1.0f + sqrt_pt(fmaf(r2, t2, 1.0f)));
 }
 
 // Core/fresnel.h:11-49 (pow(x, 2.0f) -> x*x). tir_asin = asin(out_n / in_n), precomputed per material
@@ -160,23 +171,22 @@ __device__ __forceinline__ float fresnel_dielectric(v3 n, v3 in, float in_n, flo
     float cos_out = dot(-1.0f * n, refr);
     if (in_n > out_n && acos_pt(cos_in) >= tir_asin) return 1.0f;
     if (dot(refr, refr) <= refr_len2 || cos_out < 0) return 1.0f;
-    float s = (in_n * cos_in - out_n * cos_out) / (in_n * cos_in + out_n * cos_out);
-    float p = (in_n * cos_out - out_n * cos_in) / (in_n * cos_out + out_n * cos_in);
-    float rs = s * s;
-    float rp = p * p;
-    return (rs + rp) / 2.0f;
+    float s = fmaf(in_n, cos_in, -(out_n * cos_out)) / fmaf(in_n, cos_in, out_n * cos_out);
+    float p = fmaf(in_n, cos_out, -(out_n * cos_in)) / fmaf(in_n, cos_out, out_n * cos_in);
+    return fmaf(s, s, p * p) / 2.0f;  // (s^2 + p^2) / 2
 }
 
 // Core/fresnel.h:51-76
 __device__ __forceinline__ float fresnel_conductor(v3 n, v3 in, float eta, float k) {
     float cos_in = dot(n, in * -1.0f);
-    float n2 = eta * eta;
-    float k2 = k * k;
-    float nk = n2 + k2;
+    float nk = fmaf(eta, eta, k * k);  // eta^2 + k^2
     float c2 = cos_in * cos_in;
-    float two_n_c = 2 * eta * cos_in;
-    float rs = (nk * c2 - two_n_c + 1.0f) / (nk * c2 + two_n_c + 1.0f);
-    float rp = (nk - two_n_c + c2) / (nk + two_n_c + c2);
+    float two_n = 2 * eta;
+    float two_n_c = two_n * cos_in;
+    // (nk c2 - 2 eta c + 1) / (nk c2 + 2 eta c + 1): the left product of each sum fused
+    float rs = (fmaf(nk, c2, -two_n_c) + 1.0f) / (fmaf(nk, c2, two_n_c) + 1.0f);
+    // (nk - 2 eta c + c^2) / (nk + 2 eta c + c^2): each product fused in turn
+    float rp = fmaf(cos_in, cos_in, fmaf(-two_n, cos_in, nk)) / fmaf(cos_in, cos_in, fmaf(two_n, cos_in, nk));
     return (rs + rp) / 2.0f;
 }
 
@@ -197,7 +207,7 @@ __device__ __forceinline__ unsigned int texel_raw(const uint8_t* px, int idx) {
     return *reinterpret_cast<const unsigned int*>(px + (size_t)idx * 4);
 }
 __device__ __forceinline__ float texel_c(unsigned int t, int c) { return u8_unit((t >> (8 * c)) & 0xffu); }
-__device__ __forceinline__ float lerp1(float a, float b, float t) { return a + t * (b - a); }
+__device__ __forceinline__ float lerp1(float a, float b, float t) { return fmaf(t, b - a, a); }  // lerp, contracted
 
 // Core/texture.h:15-79 (also the face lookup of Core/cube_map.h:20-119, same arithmetic)
 __device__ __forceinline__ v3 sample_rgba8(const uint8_t* px, int w, int h, float au, float av, int bilinear) {
@@ -270,7 +280,7 @@ __device__ __forceinline__ v3 background(const DevScene& sc, const DevConfig& cf
         float t = (dot(d, mk3(-0.41f, 0.41f, -0.82f)) + 1.0f) / 2.0f;
         v3 a = mk3(0.15f, 0.3f, 0.5f);
         v3 b = mk3(1.0f, 1.0f, 1.0f);
-        return ((1.0f - t) * a + t * b) * 1.0f;
+        return fma3(a, 1.0f - t, t * b) * 1.0f;  // ((1 - t) a + t b) * 1, the left product fused
     }
     return mk3(0.0f, 0.0f, 0.0f);
 }
@@ -279,7 +289,7 @@ __device__ __forceinline__ v3 background(const DevScene& sc, const DevConfig& cf
 __device__ __forceinline__ bool sphere_t(float4 s, v3 o, v3 d, float* t_out) {
     v3 op = mk3(s.x, s.y, s.z) - o;
     float b = dot(op, d);
-    float delta = b * b - dot(op, op) + s.w * s.w;
+    float delta = fmaf(s.w, s.w, fmaf(b, b, -dot(op, op)));  // (b b - op.op) + r r, contracted
     if (delta < 0) return false;
     float dr = sqrt_pt(delta);
     float t1 = b - dr;
@@ -514,7 +524,7 @@ __device__ __forceinline__ void generate_path(const DevCamera& cam, const DevCon
     ps->medium = -1;
 
     int image_y = (int)((float)pixel / cam.res_x);
-    int image_x = (int)((float)pixel - ((float)image_y * cam.res_x));
+    int image_x = (int)fmaf(-(float)image_y, cam.res_x, (float)pixel);  // pixel - image_y * res_x, contracted
     minstd rng = minstd_seed(mul_wrap(mul_wrap(hseed, hseed), hash_pt(pixel)));
     float jx = 0.0f, jy = 0.0f;
     if (cfg.use_anti_alias) {
@@ -525,10 +535,10 @@ __device__ __forceinline__ void generate_path(const DevCamera& cam, const DevCon
     v3 view = mk3(cam.view[0], cam.view[1], cam.view[2]);
     v3 xa = mk3(cam.x_axis[0], cam.x_axis[1], cam.x_axis[2]);
     v3 ya = mk3(cam.y_axis[0], cam.y_axis[1], cam.y_axis[2]);
-    float nx = (((float)image_x + jx) / (cam.res_x - 1.0f)) * 2.0f - 1.0f;
-    float ny = (((float)image_y + jy) / (cam.res_y - 1.0f)) * 2.0f - 1.0f;
-    v3 canvas = eye + view + nx * xa + ny * ya;
-    v3 image_plane = eye + normalize(canvas - eye) * cam.focal;
+    float nx = fmaf(((float)image_x + jx) / (cam.res_x - 1.0f), 2.0f, -1.0f);
+    float ny = fmaf(((float)image_y + jy) / (cam.res_y - 1.0f), 2.0f, -1.0f);
+    v3 canvas = fma3(ya, ny, fma3(xa, nx, eye + view));      // ((eye + view) + nx xa) + ny ya
+    v3 image_plane = fma3(normalize(canvas - eye), cam.focal, eye);  // eye + normalize(.) focal
     v3 ap;
     if (cam.aperture > 0.00001f) {
         float r1 = minstd_uniform(&rng, -0.5f, 0.5f) + 0.5f;
@@ -541,7 +551,7 @@ __device__ __forceinline__ void generate_path(const DevCamera& cam, const DevCon
         float ay = sa * dist;
         v3 hz = mk3(cam.horizontal[0], cam.horizontal[1], cam.horizontal[2]);
         v3 vt = mk3(cam.vertical[0], cam.vertical[1], cam.vertical[2]);
-        ap = eye + ax * hz + ay * vt;
+        ap = fma3(vt, ay, fma3(hz, ax, eye));  // (eye + ax hz) + ay vt
     } else {
         ap = eye;
     }
@@ -591,6 +601,27 @@ __device__ __forceinline__ Hit closest_hit(const DevScene& sc, v3 o, v3 d, Count
 
 // The per-path part of the trace seed hash(seed) * hash(pixel) * hash(depth) (:415), int wrap.
 __device__ __forceinline__ int32_t path_seed(int32_t hseed, int pixel) { return mul_wrap(hseed, hash_pt(pixel)); }
+
+// The medium-bounded walk (pt_set_medium_bound / PT_MEDIUM_BOUND; a tolerance mode, off by default). A segment
+// inside a scattering medium (:460-462) draws its free-flight distance first (:463-464) and scatters there
+// when it is shorter than the closest hit (:466); intersection draws nothing, so the distance is known
+// before the walk. A hit beyond it cannot matter, so each mesh walk may start with min_t = dist (1 + 2^-10)
+// instead of infinity, which prunes every box entered beyond it. This equals the reference's walk whenever
+// every box around an accepted triangle has a computed entry within that margin of the triangle's computed
+// t; Moller-Trumbore on a ray grazing the triangle's plane has no such bound, so exactness is not proven.
+// Measured: the whole C4 frame (72 M segments) renders bit-identical to the unbounded walk
+// (profiles/r04/medium_bound/). Returns the walks' starting min_t: +inf outside a scattering medium.
+__device__ __forceinline__ float medium_bound(const DevScene& sc, const DevConfig& cfg, int medium, int depth,
+                                              int32_t pseed) {
+    float sa[3], ss[3];
+    medium_coefficients(sc, cfg, medium, sa, ss);
+    if (ss[0] > 0.0f || dot(mk3(sa[0], sa[1], sa[2]), mk3(sa[0], sa[1], sa[2])) > cfg.sss_len2) {
+        minstd rng = minstd_seed(mul_wrap(pseed, hash_pt(depth)));  // shade_hit's generator, first draw
+        const float dist = -log_pt(minstd_uniform(&rng, 0.0f, 1.0f)) / ss[0];
+        if (dist >= 0.0f && dist < __builtin_inff()) return dist + dist * 0x1p-10f;
+    }
+    return __builtin_inff();
+}
 
 // Scene features shade_hit can meet (pass_kernel_u is specialised on them: code a scene cannot reach is
 // left out, which lowers the kernel's register peak). A feature left out must be unreachable for the
@@ -648,7 +679,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
             if (dist < min_t) {
                 float r1 = minstd_uniform(&rng, 0.0f, 1.0f);
                 float r2 = minstd_uniform(&rng, 0.0f, 1.0f);
-                ps->o = ps->o + ps->d * dist;
+                ps->o = fma3(ps->d, dist, ps->o);  // point_on_ray(dist) (ray.h:16), contracted
                 ps->d = sample_sphere(r1, r2);
                 ps->thr = ps->thr * absorption(sa, dist);
                 if (STATS) ctr->scatter++;
@@ -663,14 +694,14 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
     if (STATS) { ctr->miss += h.type == 0; ctr->hit_sphere += h.type == 1; ctr->hit_mesh += h.type == 2; }
     if (h.type == 0) {  // miss (:618-624)
         v3 bg = background(sc, cfg, d);
-        ps->rad = ps->rad + ps->thr * bg;
+        ps->rad = fma3v(ps->thr, bg, ps->rad);  // rad += thr * bg, contracted
         return false;
     }
 
     // material of the hit (:496-527); fields are read where they are used. The texture modulation
     // (:518-526) is applied in the branch that uses it (specular: reflect, diffuse: diffuse), from the
     // interpolated uv, so only uv stays live through Fresnel and the bounce choice.
-    const v3 point = o + d * min_t;
+    const v3 point = fma3(d, min_t, o);  // point_on_ray (ray.h:16; sphere.h:50 likewise), contracted
     v3 normal;
     int mid;
     v2 uv = mk2(0.0f, 0.0f);
@@ -689,11 +720,11 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
         mid = f2i(s3.w);
         v3 n0 = mk3(s0.x, s0.y, s0.z), n1 = mk3(s0.w, s1.x, s1.y), n2 = mk3(s1.z, s1.w, s2.x);
         float w = 1.0f - h.t1 - h.t2;
-        normal = n0 * w + n1 * h.t1 + n2 * h.t2;
+        normal = fma3(n2, h.t2, fma3(n0, w, n1 * h.t1));  // (n0 w + n1 t1) + n2 t2, contracted
         const DevMaterial& M = sc.materials[mid];
         if ((FEAT & PT_FEAT_TEX) && (M.diffuse_texture_id != -1 || M.specular_texture_id != -1)) {
             v2 uv0 = mk2(s2.y, s2.z), uv1 = mk2(s2.w, s3.x), uv2 = mk2(s3.y, s3.z);
-            uv = uv0 * w + uv1 * h.t1 + uv2 * h.t2;
+            uv = mk2(fmaf(uv2.x, h.t2, fmaf(uv0.x, w, uv1.x * h.t1)), fmaf(uv2.y, h.t2, fmaf(uv0.y, w, uv1.y * h.t1)));
             textured = true;
         }
     }
@@ -743,7 +774,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
         // both branches take sqrtf(r1) and one more square root: computed once for the batch, with the
         // second one's argument chosen per lane (a batch holds lanes of both kinds)
         const float s1 = sqrt_pt(r1);
-        const float s2 = sqrt_pt(reflect ? 1.0f - r1 : 1.0f - s1 * s1);
+        const float s2 = sqrt_pt(reflect ? 1.0f - r1 : fmaf(-s1, s1, 1.0f));
         float cos_t, sin_t;
         if (reflect) {  // sample_on_hemisphere_ggx_weight (:194-223), alpha = roughness^1.85 * 0.238 (:571)
             const float theta = atan_pt(M.rough_alpha * s1 / s2);  // alpha * sqrtf(r1) / sqrtf(1 - r1)
@@ -767,7 +798,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
             v3 diff = mk3(M.diffuse[0], M.diffuse[1], M.diffuse[2]);
             if (textured && M.diffuse_texture_id != -1)
                 diff = diff * sample_texture(sc, M.diffuse_texture_id, uv, cfg.use_bilinear);
-            ps->rad = ps->rad + ps->thr * mk3(M.emission[0], M.emission[1], M.emission[2]);
+            ps->rad = fma3v(ps->thr, mk3(M.emission[0], M.emission[1], M.emission[2]), ps->rad);  // +=, contracted
             ps->thr = ps->thr * diff;
             ps->o = point + bias_v;
             ps->d = dir;

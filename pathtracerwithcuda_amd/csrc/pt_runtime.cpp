@@ -483,6 +483,7 @@ struct pt_context {
     bool instrumented = false;
     int schedule = -1;  // PT_SCHEDULE_*; -1: environment default (PT_MODE)
     int grid_share = 100;   // pt_set_grid_share: percent of the occupancy-sized grid a pass launch takes
+    int medium_bound = -1;  // pt_set_medium_bound: -1 = PT_MEDIUM_BOUND from the environment (default off)
     // pt_set_band_order / pt_band_cost: the order in which this context's bands are handed out, and
     // per-band ray-segment counters (allocated while measuring); both for the current tiling only
     int* band_order = nullptr;
@@ -936,6 +937,14 @@ bool wavefront_schedule(const pt_context* ctx) {
     return ctx->schedule == PT_SCHEDULE_WAVEFRONT || (ctx->schedule < 0 && use_wavefront());
 }
 
+int env_medium_bound() {
+    static const int v = [] {
+        const char* e = getenv("PT_MEDIUM_BOUND");
+        return (e && std::strcmp(e, "1") == 0) ? 1 : 0;
+    }();
+    return v;
+}
+
 int prepare_launch(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config, LaunchParams& lp) {
     if (!ctx->has_scene) { set_error("no scene uploaded"); return PT_E_STATE; }
     if (!ctx->image) { set_error("no frame set up"); return PT_E_STATE; }
@@ -959,6 +968,7 @@ int prepare_launch(pt_context* ctx, const pt_render_camera* cam, const pt_config
         lp.sc.first_range = ctx->il_first;
     }
     lp.cfg = dc;
+    lp.cfg.medium_bound = ctx->medium_bound >= 0 ? ctx->medium_bound : env_medium_bound();
     lp.cam = dcam;
     lp.til = ctx->tiling;
     const int nb = (ctx->band_order || ctx->band_cost_on) ? local_bands(ctx, nullptr) : 0;
@@ -1331,6 +1341,12 @@ extern "C" int pt_scene_info(pt_context* ctx, long long* bytes, int* node_num, i
     if (bytes) *bytes = (long long)ctx->scene_bytes;
     if (node_num) *node_num = ctx->node_num;
     if (triangle_num) *triangle_num = ctx->tri_num;
+    return PT_OK;
+}
+
+extern "C" int pt_set_medium_bound(pt_context* ctx, int on) {
+    if (!ctx || on < -1 || on > 1) { set_error("bad medium bound switch"); return PT_E_ARG; }
+    ctx->medium_bound = on;
     return PT_OK;
 }
 

@@ -106,6 +106,9 @@ struct DevConfig {
     float energy_len2;  // energy_exist_threshold (the kill test, path_tracer_kernel.cu:612-616)
     float sss_len2;     // sss_threshold (:460)
     float refr_len2;    // 0.000005f (fresnel.h:37, length(refraction) <= 0.000005f)
+    // pt_set_medium_bound (tolerance mode, off by default): pass_kernel_u walks an in-medium segment's meshes
+    // with min_t starting at its free-flight distance (1 + 2^-10) instead of infinity (pt_path.h medium_bound)
+    int medium_bound;
 };
 
 // Core/camera.h:14-23 plus the per-frame canvas terms generate_ray_kernel derives

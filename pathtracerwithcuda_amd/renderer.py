@@ -99,6 +99,11 @@ class Renderer:
         v = self._lib.pt_last_kernel(self._ctx)
         return v.decode() if v else ""
 
+    def set_medium_bound(self, on) -> None:
+        """Tolerance mode: in-medium segments walk with min_t starting at their free-flight distance
+        (pt_set_medium_bound; None = the PT_MEDIUM_BOUND environment variable, the default: off)."""
+        check(self._lib.pt_set_medium_bound(self._ctx, -1 if on is None else int(bool(on))), "pt_set_medium_bound")
+
     def set_grid_share(self, percent: int) -> None:
         """Percentage of the occupancy-sized grid this context's pass launches take (frames in flight)."""
         check(self._lib.pt_set_grid_share(self._ctx, int(percent)), "pt_set_grid_share")

@@ -410,6 +410,54 @@ def test_c4_800k_sss_frame(bench_gpu, c4_workload):
     assert launches == {0: 1, 3: 1}, launches
 
 
+def test_medium_bound_mode_c4_frame(bench_gpu, c4_workload):
+    """The medium-bounded walk (pt_set_medium_bound, a tolerance mode off by default; pt_path.h medium_bound):
+    in-medium segments walk with min_t starting at their free-flight distance. The whole C4 frame through it
+    equals the oracle's bounded walk bit for bit, and the bounded walk stays within the stated tolerance of
+    the reference's unbounded one (measured identical on the whole frame)."""
+    wl = c4_workload
+    r = bench_gpu
+    r.set_medium_bound(True)
+    try:
+        r.upload(wl.scene, wl.cfg)
+        r.setup_frame(wl.width, wl.height)
+        r.render(wl.cam, wl.cfg, 1, 8, write_u8=2)
+        img, img8 = r.download()
+        assert r.last_kernel().startswith("pass_kernel_u"), r.last_kernel()
+    finally:
+        r.set_medium_bound(None)
+    ref, ref8, sb = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, 8, medium_bound=True)
+    assert_bitwise(img.reshape(-1, 3), ref, "bounded C4 float")
+    assert_bitwise(img8.reshape(-1, 3), ref8, "bounded C4 8-bit")
+    exact, _, se = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, 8)
+    assert sb["nodes"] < 0.8 * se["nodes"], (sb["nodes"], se["nodes"])  # the walk really is bounded
+    d = np.abs(ref.astype(np.float64) - exact).max(axis=1)
+    assert (d <= 1e-3).mean() >= 0.998 and (d > 1e-3).mean() <= 0.001, f"{(d > 0).sum()} pixels differ"
+
+
+def test_medium_bound_mode_variants(bench_gpu):
+    """The bounded walk on the small subsurface scene and with a scattering air (every segment in a medium)."""
+    r = bench_gpu
+    for sc, cfg_kw in ((pt.cornell_scene(pt.torus_knot(60, 16), mesh_material="DragonGreen", cube_length=32),
+                        dict(max_tracer_depth=10)),
+                       (pt.cornell_scene(pt.torus_knot(40, 12), cube_length=32),
+                        dict(max_tracer_depth=8, air_absorption_coef=(0.02, 0.03, 0.05),
+                             air_reduced_scattering_coef=(0.05, 0.05, 0.05)))):
+        cfg = pt.configuration(**cfg_kw)
+        cam = pt.camera(72, 40, **BENCH_CAM)
+        r.set_medium_bound(True)
+        try:
+            r.upload(sc, cfg)
+            r.setup_frame(72, 40)
+            r.render(cam, cfg, 1, 2, write_u8=2)
+            img, img8 = r.download()
+        finally:
+            r.set_medium_bound(None)
+        ref, ref8, _ = oracle.render(sc.view, cam, cfg, 1, 2, medium_bound=True)
+        assert_bitwise(img.reshape(-1, 3), ref, "bounded variant float")
+        assert_bitwise(img8.reshape(-1, 3), ref8, "bounded variant 8-bit")
+
+
 def test_c5_4k_textured_depth12_frame(bench_gpu):
     """BASELINE config C5: three textured knots + a textured cube (diffuse and specular maps) at 3840x2160,
     depth 12, 8 passes in one launch, whole frame (8.3 M pixels) against the oracle."""
@@ -661,7 +709,7 @@ def test_reference_abi_alternates_with_cpu_twin_on_managed_buffers(require_gpu):
     """Core/path_tracer.cpp:40-91 picks the GPU entry or the CPU twin path_tracer_cpu per pass, on the
     SAME managed image (Core/image.cpp:15-27) and scratch (path_tracer_kernel.cu:782-796) buffers. Here
     passes 1, 3, 4 run through path_tracer_kernel and passes 2, 5 are the CPU twin (the oracle in the
-    reference CPU-fallback mode: MSVC rand, libm) writing the managed buffers on the host. Every GPU
+    reference CPU-fallback mode: MSVC rand, libm, unfused arithmetic) writing the managed buffers on the host. Every GPU
     pass must add into what the host left there: the result equals the same five-pass chain run by
     the oracle alone, bit for bit."""
     sc = pt.cornell_scene(pt.torus_knot(50, 14), cube_length=32)
@@ -696,8 +744,8 @@ def test_reference_abi_alternates_with_cpu_twin_on_managed_buffers(require_gpu):
                 oracle.render(v, cam, cfg, p, 1, image=want, image256=want8)
             else:
                 assert hip.hipDeviceSynchronize() == 0
-                oracle.render(v, cam, cfg, p, 1, rng="msvc", math="libm", image=img, image256=img8)
-                oracle.render(v, cam, cfg, p, 1, rng="msvc", math="libm", image=want, image256=want8)
+                oracle.render(v, cam, cfg, p, 1, rng="msvc", math="libm", arith="plain", image=img, image256=img8)
+                oracle.render(v, cam, cfg, p, 1, rng="msvc", math="libm", arith="plain", image=want, image256=want8)
         assert hip.hipDeviceSynchronize() == 0
         assert_bitwise(img.reshape(-1, 3), want, "alternating GPU/CPU float")
         assert_bitwise(img8.reshape(-1, 3), want8, "alternating GPU/CPU 8-bit")

@@ -108,7 +108,8 @@ def test_oracle_pass_accumulation_and_threads(small_scene):
 @pytest.fixture(scope="module")
 def metric_subset():
     """BASELINE.json's metric frame (1920x1080, 70k-triangle knot, depth 8, 8 passes) on a 20,000-pixel
-    subset, rendered by the bit-exact restatement (Cephes transcendentals, no contraction)."""
+    subset, rendered by the bit-exact restatement (Cephes transcendentals, the CUDA build's contraction
+    sites as fused multiply-adds)."""
     import bench
     wl = bench.Workload("metric")
     sel = np.sort(np.random.default_rng(1).choice(wl.width * wl.height, 20000, replace=False)).astype(np.int32)
@@ -119,36 +120,47 @@ def metric_subset():
 @pytest.fixture(scope="module")
 def c4_subset():
     """BASELINE.json's C4 frame (800k-triangle knot, DragonGreen subsurface medium, depth 8, 8 passes) on a
-    3,000-pixel subset: the configuration where __powf(E, -sigma_a d) (path_tracer_kernel.cu:245-247) meets
+    12,000-pixel subset: the configuration where __powf(E, -sigma_a d) (path_tracer_kernel.cu:245-247) meets
     large exponents (sigma_a = 40)."""
     import bench
     wl = bench.Workload("c4")
-    sel = np.sort(np.random.default_rng(4).choice(wl.width * wl.height, 3000, replace=False)).astype(np.int32)
+    sel = np.sort(np.random.default_rng(4).choice(wl.width * wl.height, 12000, replace=False)).astype(np.int32)
     a, _, sa = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, 8, pixels=sel, signatures=True)
     return wl, sel, a, sa["signatures"]
 
 
-MODELS = {"libm": dict(math="libm"), "fma": dict(variant="fma"), "fma+libm": dict(variant="fma", math="libm"),
-          "cuda": dict(math="cuda"), "cuda_site": dict(math="cuda_site"), "fma+cuda": dict(variant="fma", math="cuda"),
-          "fma+cuda_site": dict(variant="fma", math="cuda_site")}
+MODELS = {"libm": dict(math="libm"), "plain": dict(arith="plain"), "plain+libm": dict(arith="plain", math="libm"),
+          "fma": dict(variant="fma"), "cuda": dict(math="cuda"), "cuda_site": dict(math="cuda_site"),
+          "plain+cuda": dict(arith="plain", math="cuda"), "plain+cuda_site": dict(arith="plain", math="cuda_site")}
 
 
 def _assert_within_stated_tolerance(subset, model):
-    """The stated tolerance, per pixel of the 8-pass running sum: >= 99.8 % of pixels within
-    1e-3 per channel, RMSE <= 2e-2 x the mean, |mean shift| <= 5e-5 x the mean, no NaN/Inf, a path-topology
-    change (hit primitive, branch, sky face) in <= 3 % of pixels, and <= 0.1 % of pixels beyond 1e-3 without
-    such a change."""
+    """The stated tolerance, per pixel of the 8-pass running sum: no NaN/Inf; >= 99.8 % of
+    pixels within 1e-3 per channel; a path-topology change (hit primitive, branch, sky face: a resample of
+    the path) in <= 3 % of pixels; <= 0.1 % of pixels beyond 1e-3 without such a change; and over the
+    pixels without one (rounding differences only) a relative difference (per channel, against
+    max(|ref|, 1e-3)) <= 1e-4 at the 99th percentile and <= 2e-3 at the 99.9th. (Whole-frame means, flips
+    included, stay within 1.6e-5 x the mean, profiles/r04/fma/tolerance_*_whole.txt; RMSE and mean over a
+    pixel sample are not stated: one flipped firefly, or one ill-conditioned grazing GGX pixel, moves them.)"""
     wl, sel, a, sig_a = subset
     b, _, sb = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, 8, pixels=sel, signatures=True, **MODELS[model])
     assert np.isfinite(b).all() and np.isfinite(a).all()
-    d = np.abs(a.astype(np.float64) - b).max(axis=1)
+    diff = b.astype(np.float64) - a
+    d = np.abs(diff).max(axis=1)
     flipped = (sig_a != sb["signatures"]).any(axis=0)
+    clean = ~flipped
     assert (d <= 1e-3).mean() >= 0.998
-    assert np.sqrt(np.mean((a.astype(np.float64) - b) ** 2)) <= 2e-2 * a.mean()
-    assert abs(float(b.mean()) - float(a.mean())) <= 5e-5 * float(a.mean())
     assert flipped.mean() <= 0.03
-    assert ((d > 1e-3) & ~flipped).sum() <= 0.001 * len(sel)
-    assert flipped.any()  # the models do perturb the paths (the test is not vacuous)
+    assert ((d > 1e-3) & clean).sum() <= 0.001 * len(sel)
+    rel = (np.abs(diff) / np.maximum(np.abs(a), 1e-3)).max(axis=1)[clean]
+    assert np.percentile(rel, 99) <= 1e-4 and np.percentile(rel, 99.9) <= 2e-3
+    if model == "fma":
+        # gcc's own contraction (-ffp-contract=fast) of the whole oracle finds the explicit fmaf sites and
+        # only adds ones inside the Cephes stand-ins: >= 99 % of pixels the same bits (whole metric frame:
+        # 99.82 %, 25 of 2.07 M pixels with a flipped path; profiles/r04/fma/tolerance_metric_whole.txt)
+        assert flipped.mean() <= 0.001 and (d == 0).mean() >= 0.99
+    else:
+        assert flipped.any()  # the models do perturb the paths (the test is not vacuous)
 
 
 @pytest.mark.parametrize("model", list(MODELS))
@@ -156,20 +168,19 @@ def test_tolerance_to_a_cuda_like_build(metric_subset, model):
     """The stated per-pixel tolerance against the reference CUDA renderer. The CUDA build
     cannot run here; what separates it from this bit-exact restatement is (a) its hardware intrinsics
     __sinf/__cosf/__tanf/__expf/__logf/__powf and rsqrtf (path_tracer_kernel.cu:191,203-204,222,235,
-    245-247,344-345,364-365,464,571,595,660-662; cuda_math.hpp:1458) and (b) nvcc's default FMA
-    contraction. Models on the same frame: glibc's transcendentals ("libm"), the documented maximum error
-    of every intrinsic ("cuda", oracle_math.h OR_MATH_CUDA; "cuda_site" keys the error's direction by
-    (pass, pixel, depth, call)), the oracle compiled with -ffp-contract=fast ("fma"), and the combinations.
-    Measured (20,000 pixels, 8 passes, profiles/r03/tolerance_metric.txt): >= 99.89 % within 1e-3,
-    RMSE <= 1.05e-2 x the mean, |mean shift| <= 1.1e-5, topology changes in <= 2.1 % of pixels, <= 12
-    pixels beyond 1e-3 without one; the intrinsic models are the far end."""
+    245-247,344-345,364-365,464,571,595,660-662; cuda_math.hpp:1458) and (b) which products nvcc's
+    contraction actually fuses (the restatement fuses them by a stated rule). Models on the
+    same frame: glibc's transcendentals ("libm"), the documented maximum error of every intrinsic ("cuda",
+    oracle_math.h OR_MATH_CUDA; "cuda_site" keys the error's direction by (pass, pixel, depth, call)), no
+    contraction at all ("plain": an nvcc --fmad=false build), gcc's own contraction of the whole oracle
+    ("fma"), and the combinations. Whole-frame measurements: profiles/r04/fma/tolerance_metric_whole.txt."""
     _assert_within_stated_tolerance(metric_subset, model)
 
 
-@pytest.mark.parametrize("model", ["cuda", "fma+cuda", "cuda_site"])
+@pytest.mark.parametrize("model", ["cuda", "plain+cuda", "cuda_site"])
 def test_tolerance_to_a_cuda_like_build_c4(c4_subset, model):
-    """The same stated tolerance at C4 (profiles/r03/tolerance_c4.txt): the large-exponent __powf of the
-    subsurface medium stays inside it (max relative change of an unflipped pixel 1.3e-3)."""
+    """The same stated tolerance at C4 (profiles/r04/fma/tolerance_c4_whole.txt): the large-exponent __powf
+    of the subsurface medium stays inside it."""
     _assert_within_stated_tolerance(c4_subset, model)
 
 

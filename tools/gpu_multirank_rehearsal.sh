@@ -1,8 +1,22 @@
-# Rehearsal of the N > 1 bench path on a one-GPU box: 2 and 4 ranks (gather), 3 ranks (reduce) over gloo,
-# every rank on device 0; the 8-bit images after several frames must equal the 1-GPU image.
-mkdir -p gpurun_out/mr
-timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --save-image gpurun_out/mr/n1.png > gpurun_out/mr/b1.json 2>/dev/null || exit $?
-PT_BENCH_BACKEND=gloo PT_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --save-image gpurun_out/mr/n2.png > gpurun_out/mr/b2.json 2> gpurun_out/mr/b2.err || exit $?
-PT_FRAME_COLLECTIVE=reduce PT_BENCH_BACKEND=gloo PT_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 3 --steps 2 --warmup 1 --save-image gpurun_out/mr/n3r.png > gpurun_out/mr/b3.json 2> gpurun_out/mr/b3.err || exit $?
-PT_BENCH_BACKEND=gloo PT_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 4 --steps 3 --warmup 1 --save-image gpurun_out/mr/n4.png > gpurun_out/mr/b4.json 2> gpurun_out/mr/b4.err || exit $?
-cmp gpurun_out/mr/n1.png gpurun_out/mr/n2.png && cmp gpurun_out/mr/n1.png gpurun_out/mr/n3r.png && cmp gpurun_out/mr/n1.png gpurun_out/mr/n4.png && echo "images identical"
+# Rehearsal of the N > 1 bench path on a one-GPU box: 2, 4 and 8 ranks gathering and 3 reducing over gloo,
+# every rank on device 0. Each bench line carries config.image_matches_1gpu (rank 0 re-renders the frame
+# alone and compares bitwise) and bench.py exits 3 on a mismatch; the saved 8-bit images must also equal the
+# 1-GPU image.
+#   gpurun --timeout 900 -- bash tools/gpu_multirank_rehearsal.sh [tag]
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+TAG=${1:-mr}
+mkdir -p gpurun_out/$TAG
+timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --save-image gpurun_out/$TAG/n1.png > gpurun_out/$TAG/b1.json 2>/dev/null || exit $?
+run() {  # ranks port extra-env...
+  n=$1; port=$2; shift 2
+  env "$@" PT_BENCH_BACKEND=gloo PT_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $port bench.py --gpus $n --steps 3 --warmup 1 --save-image gpurun_out/$TAG/n$n.png > gpurun_out/$TAG/b$n.json 2> gpurun_out/$TAG/b$n.err || exit $?
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], 'ranks: image_matches_1gpu', d['config']['image_matches_1gpu'], d['value'], 'Mrays/s')" gpurun_out/$TAG/b$n.json $n
+  cmp gpurun_out/$TAG/n1.png gpurun_out/$TAG/n$n.png || exit 4
+}
+run 2 29533 PT_FRAME_COLLECTIVE=gather
+run 3 29534 PT_FRAME_COLLECTIVE=reduce
+run 4 29535 PT_FRAME_COLLECTIVE=gather
+run 8 29536 PT_FRAME_COLLECTIVE=gather
+echo "saved images identical to the 1-GPU image"
