@@ -559,7 +559,7 @@ __device__ __forceinline__ void generate_path(const DevCamera& cam, const DevCon
     ps->d = normalize(image_plane - ap);
 }
 
-// The kill test (path_tracer_kernel.cu:612-616, and :484-487 after a scatter): the reference ends a path
+// The kill test (path_tracer_kernel.cu:612-616, and :479-483 after a scatter): the reference ends a path
 // iff length(thr) <= energy_exist_threshold, so a NaN throughput (NaN <= x is false) keeps the path going.
 // Tested as !(dot(thr, thr) <= energy_len2), the same unordered outcome (DevConfig::energy_len2).
 __device__ __forceinline__ bool alive_after(v3 thr, const DevConfig& cfg) {

@@ -7,7 +7,10 @@ Each call ends with the running sum and the 8-bit image in the caller's buffers.
 bench scene; the first frame (scene translation and upload) is excluded; the camera moves between
 frames and every frame's pass 1 re-checks the scene (the reference resets pass_counter after a move).
 
-    python tools/abi_rate.py [--frames F] [--image managed|host]
+    python tools/abi_rate.py [--frames F] [--image managed|host] [--moving]
+
+--moving: the window while the user drags the camera (window.cpp:194-215): every call is pass 1 of a new
+camera (the orbit turns by 1e-3 rad per call); reports ms per call.
 """
 import argparse
 import ctypes as C
@@ -27,6 +30,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=4)
     ap.add_argument("--image", choices=["managed", "host"], default="managed")
+    ap.add_argument("--moving", action="store_true")
     args = ap.parse_args()
     wl = bench.Workload("metric")
     v, cam, cfg = wl.scene.view, wl.cam, wl.cfg
@@ -62,6 +66,22 @@ def main() -> None:
 
     frame(cams[1])  # scene translation + upload on the first pass
     per_pass[:] = [0.0] * (wl.spp + 1)
+    if args.moving:
+        calls = max(8, args.frames * wl.spp)
+        moving = [pt.camera(wl.width, wl.height, yaw=1e-3 * (i + 2), **bench.CAMERA) for i in range(calls)]
+        t0 = time.perf_counter()
+        for c in moving:
+            lib.path_tracer_kernel(v.mesh_num, v.bvh_nodes, v.triangles, v.sphere_num, v.spheres, n, img, img8, 1,
+                                   C.byref(c), v.sky_cube_map, *scratch, v.mesh_textures, C.byref(cfg))
+        dt = (time.perf_counter() - t0) / calls
+        lib.path_tracer_kernel_memory_free(*scratch)
+        if hip is not None:
+            hip.hipFree(pimg)
+            hip.hipFree(pimg8)
+        print(json.dumps({"path": f"path_tracer_kernel (reference ABI, {args.image} image buffers), camera moving: "
+                                  "every call is pass 1 of a new camera", "ms_per_call": round(dt * 1000, 3),
+                          "calls": calls}), flush=True)
+        return
     t0 = time.perf_counter()
     for f in range(args.frames):
         frame(cams[f % 2])

@@ -12,7 +12,7 @@ timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --save-
 run() {  # ranks port extra-env...
   n=$1; port=$2; shift 2
   env "$@" PT_BENCH_BACKEND=gloo PT_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $port bench.py --gpus $n --steps 3 --warmup 1 --save-image gpurun_out/$TAG/n$n.png > gpurun_out/$TAG/b$n.json 2> gpurun_out/$TAG/b$n.err || exit $?
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], 'ranks: image_matches_1gpu', d['config']['image_matches_1gpu'], d['value'], 'Mrays/s')" gpurun_out/$TAG/b$n.json $n
+  python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], 'ranks: image_matches_1gpu', d['config']['image_matches_1gpu'], d['value'], 'Mrays/s')" gpurun_out/$TAG/b$n.json $n
   cmp gpurun_out/$TAG/n1.png gpurun_out/$TAG/n$n.png || exit 4
 }
 run 2 29533 PT_FRAME_COLLECTIVE=gather
