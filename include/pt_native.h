@@ -52,11 +52,6 @@ int pt_set_grid_share(pt_context* ctx, int percent);
  * (a ray grazing a triangle's plane can make Moller-Trumbore's t fall below its box's entry); measured
  * bit-identical on the whole C4 frame. Other schedules ignore it. */
 int pt_set_medium_bound(pt_context* ctx, int on);
-/* Path hand-over (-1 = the PT_SPILL environment variable, default 0 = off): once a pass
- * launch's work is drained, a wave holding at most k paths hands each of them over at its next segment start
- * (64 B in HBM) and ends; a follow-up launch on a share of the grid carries them on densely packed. Results
- * do not depend on it (a path's draws are keyed by (pass, pixel, depth)). */
-int pt_set_spill(pt_context* ctx, int k);
 /* Band order of the work queue. The context's pixels are bands of band_rows rows
  * (pt_set_tiling; one context: bands of the whole frame). pt_band_count gives their number and whether
  * the last is partial; pt_set_band_order(order, n) hands out local band order[i] i-th (a permutation

@@ -192,7 +192,6 @@ _PROTOS = {
     "pt_scene_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong), c_int_p, c_int_p]),
     "pt_set_grid_share": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_medium_bound": (C.c_int, [C.c_void_p, C.c_int]),
-    "pt_set_spill": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_band_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "pt_set_band_order": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.c_int]),
     "pt_band_cost_enable": (C.c_int, [C.c_void_p, C.c_int]),

@@ -31,11 +31,8 @@ hipError_t launch_inline_leaves(const float4* nodes, const float4* tri_geom, con
                                 hipStream_t stream);
 // the cube map's RGBA8 texels as float4 {u8_unit(r), u8_unit(g), u8_unit(b), 0} (DevScene::cube_f)
 hipError_t launch_cube_float(const uint8_t* cube, int texels, float4* out, hipStream_t stream);
-// hand: path hand-over instance (pass_kernel_u HAND; 0 none, 1 pass launch, 2 follow-up launch)
 hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int first_pass, int batch_log2,
-                       int write_u8, int grid, int lds_bytes, hipStream_t stream, int hand = 0);
-// whether launch_pass has the hand-over instances for this choice
-bool pass_hand_supported(const PassChoice& pc, int lds_bytes);
+                       int write_u8, int grid, int lds_bytes, hipStream_t stream);
 hipError_t launch_accumulate(const LaunchParams* params_dev, int units, int first_pass, int batch_log2, int write_u8,
                              hipStream_t stream);
 hipError_t launch_accumulate_one(const LaunchParams* params_dev, int unit_begin, int unit_end, int pass, int batch_log2,

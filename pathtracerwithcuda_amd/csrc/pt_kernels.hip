@@ -312,9 +312,7 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
 // batches, lanes in triangle batches, lanes refilled, then cycles and the drained/ready/idle counts,
 // and the launch timeline in stats[32..41].
 // FEAT: the scene features shade_hit can reach (pt_path.h PT_FEAT_*).
-// HAND: path hand-over (DevOutput::spill): 0 none, 1 the pass launch (drained waves hand their paths over),
-// 2 the follow-up launch (its units are the handed-over paths)
-template <int MINW, bool PROF, int FEAT, int HAND = 0>
+template <int MINW, bool PROF, int FEAT>
 __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
                                                                 int walk_steps, int tri_min, int walk_min) {
@@ -370,10 +368,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     float wbound = __builtin_inff();  // every mesh walk's starting min_t (medium-bounded mode only)
     unsigned long long segments = 0;  // wave-uniform: lanes shaded (ray segments traced)
     Counters none = {0u, 0u, 0u, 0u, 0u, 0u};
-    // the follow-up launch of a path hand-over takes the records its pass launch wrote (that launch has ended:
-    // same stream), otherwise the (pixel, pass) units of the batch
-    const unsigned int units = HAND == 2 ? load_const(P0->out.spill_count)  // a scalar load: wave-uniform
-                                         : (unsigned int)P0->til.unit_count << batch_log2;
+    const unsigned int units = (unsigned int)P0->til.unit_count << batch_log2;
     const EvenRegions regions{units, (units + PT_SHARDS - 1) / PT_SHARDS};
     WorkCursor cursor = work_begin();
     bool drained = false;
@@ -415,19 +410,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 gen_batches += started ? 1ull : 0ull;
             }
             if (PROF && drained && t_drain == 0) t_drain = __builtin_amdgcn_s_memrealtime();
-            if (HAND == 2 && want) {
-                if (u != ~0u) {  // a handed-over path, at the start of its next segment
-                    const float4* rec = out.spill + 4 * (size_t)u;
-                    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
-                    ps.o = mk3(r0.x, r0.y, r0.z); ps.medium = f2i(r0.w);
-                    ps.d = mk3(r1.x, r1.y, r1.z); depth = f2i(r1.w);
-                    ps.thr = mk3(r2.x, r2.y, r2.z); pseed = f2i(r2.w);
-                    ps.rad = mk3(r3.x, r3.y, r3.z); unit = (unsigned int)f2i(r3.w);
-                    mode = LANE_NEW;
-                } else if (drained) {
-                    mode = LANE_DONE;
-                }
-            } else if (want) {
+            if (want) {
                 if (u != ~0u) {
                     unit = u;
                     const int pixel = unit_to_pixel(til, u >> batch_log2);
@@ -448,26 +431,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                         finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
                     }
                 } else if (drained) {
-                    mode = LANE_DONE;
-                }
-            }
-        }
-        // path hand-over (DevOutput::spill): a drained wave with at most spill_k paths left writes every path
-        // that is about to start a segment to the records and retires the lane; the wave ends once all have
-        if (HAND == 1 && drained) {
-            const unsigned long long live = __ballot(mode != LANE_WANT && mode != LANE_DONE);
-            const unsigned long long sp = __ballot(mode == LANE_NEW);
-            if (sp && __popcll(live) <= (unsigned int)out.spill_k) {
-                const int first = (int)__builtin_ctzll(sp);
-                unsigned int base = 0;
-                if (lane == first) base = atomicAdd(out.spill_count, (unsigned int)__popcll(sp));
-                base = (unsigned int)__shfl((int)base, first);
-                if (mode == LANE_NEW) {
-                    float4* rec = out.spill + 4 * (size_t)(base + (unsigned int)__popcll(sp & lanes_below(lane)));
-                    rec[0] = make_float4(ps.o.x, ps.o.y, ps.o.z, __int_as_float(ps.medium));
-                    rec[1] = make_float4(ps.d.x, ps.d.y, ps.d.z, __int_as_float(depth));
-                    rec[2] = make_float4(ps.thr.x, ps.thr.y, ps.thr.z, __int_as_float(pseed));
-                    rec[3] = make_float4(ps.rad.x, ps.rad.y, ps.rad.z, __int_as_float((int)unit));
                     mode = LANE_DONE;
                 }
             }
@@ -893,22 +856,13 @@ using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int,
 // pass_kernel_u specialised on the scene's features (pt_path.h PT_FEAT_*): feat is what the scene can reach;
 // PT_FEAT_SPECIALISE=0 keeps the all-features kernel. `feat_used` receives the instance's features, so the
 // kernel description names the kernel that runs. PT_UPROF=1: the profiling instance (6 waves, all features).
-static PassFnU pass_fn_u(int minw, int feat, int* feat_used, int* minw_used, int hand = 0) {
+static PassFnU pass_fn_u(int minw, int feat, int* feat_used, int* minw_used) {
     static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
     static const int prof = env_int("PT_UPROF", 0, 0, 1);
     if (!spec) feat = PT_FEAT_ALL;
     if (prof) { *feat_used = PT_FEAT_ALL; *minw_used = 6; return pass_kernel_u<6, true, PT_FEAT_ALL>; }
     *feat_used = feat;
     *minw_used = minw;
-    // the hand-over instances exist for each feature set at its default wave count (pass_min_waves)
-#define PT_H_CASE(W, F) case W * 4 + F: return hand == 1 ? pass_kernel_u<W, false, F, 1> : pass_kernel_u<W, false, F, 2>;
-    if (hand) {
-        switch (minw * 4 + feat) {
-            PT_H_CASE(7, 0) PT_H_CASE(6, 1) PT_H_CASE(7, 2) PT_H_CASE(6, 3)
-            default: break;
-        }
-    }
-#undef PT_H_CASE
 #define PT_U_CASE(W, F) case W * 4 + F: return pass_kernel_u<W, false, F>;
     switch (minw * 4 + feat) {
         PT_U_CASE(5, 0) PT_U_CASE(5, 1) PT_U_CASE(5, 2) PT_U_CASE(5, 3)
@@ -933,15 +887,6 @@ static bool use_unified(const PassChoice& pc, int lds_bytes) {
 }
 
 bool pass_uses_unified(const PassChoice& pc, int lds_bytes) { return use_unified(pc, lds_bytes); }
-
-// Whether the path hand-over instances exist for this choice (pass_fn_u: the default wave count per feature
-// set, no profiling instance).
-bool pass_hand_supported(const PassChoice& pc, int lds_bytes) {
-    if (!use_unified(pc, lds_bytes) || env_int("PT_UPROF", 0, 0, 1) || !env_int("PT_FEAT_SPECIALISE", 1, 0, 1))
-        return false;
-    const int w = pass_min_waves(true, pc.feat);
-    return w == ((pc.feat & PT_FEAT_MEDIUM) ? 6 : 7);
-}
 
 // The inline-leaf copy of the node array that pass_kernel_u walks (pt_path.h walk_box_inline): record k of
 // `nodes` goes to record np[k] of `out`; a leaf (slot >= 0, one triangle per leaf) takes two records,
@@ -988,7 +933,7 @@ hipError_t launch_inline_leaves(const float4* nodes, const float4* tri_geom, con
 }
 
 hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int first_pass, int batch_log2,
-                       int write_u8, int grid, int lds_bytes, hipStream_t stream, int hand) {
+                       int write_u8, int grid, int lds_bytes, hipStream_t stream) {
     if (use_unified(pc, lds_bytes)) {
         // 64-unit chunks, a 28-lane shading batch, 7 walk steps per round, triangle batches of 6 lanes:
         // measured best with frames in flight (7 steps since the end of round 3: metric
@@ -999,7 +944,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
         static const int tri_min = env_int("PT_TRI_MIN", 6, 1, 64);
         static const int walk_min = env_int("PT_WALK_MIN", 8, 0, 64);
         int fu, wu;
-        const PassFnU fn = pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, &fu, &wu, hand);
+        const PassFnU fn = pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, &fu, &wu);
         const LaunchParams* a0 = params_dev;
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
             a8 = walk_min;

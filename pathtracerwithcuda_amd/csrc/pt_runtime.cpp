@@ -504,12 +504,6 @@ struct pt_context {
     // batched passes of the single-kernel schedule: clamped radiance per (unit, pass)
     float* pass_rad = nullptr;
     size_t pass_rad_bytes = 0;
-    // path hand-over between a pass launch and its follow-up (pt_set_spill, DevOutput::spill)
-    int spill_k = -1;                   // -1: PT_SPILL from the environment
-    float4* spill = nullptr;            // records (64 B each)
-    size_t spill_cap = 0;               // records spill can hold
-    unsigned int* spill_count = nullptr;
-    LaunchParams* params2 = nullptr;    // the follow-up launch's parameter block
     // thread_shrink scratch
     int* shrink_buf = nullptr;
     int* shrink_tiles = nullptr;
@@ -948,17 +942,6 @@ bool wavefront_schedule(const pt_context* ctx) {
     return ctx->schedule == PT_SCHEDULE_WAVEFRONT || (ctx->schedule < 0 && use_wavefront());
 }
 
-// Path hand-over threshold (pt_set_spill; PT_SPILL): 0 = off.
-int spill_threshold(const pt_context* ctx) {
-    static const int env = env_int("PT_SPILL", 0, 0, 64);
-    return ctx->spill_k >= 0 ? ctx->spill_k : env;
-}
-// The follow-up launch's share of the pass launch's grid (PT_SPILL_GRID, percent).
-int spill_grid(int g) {
-    static const int pct = env_int("PT_SPILL_GRID", 25, 1, 100);
-    return std::max(1, (int)((long long)g * pct / 100));
-}
-
 int env_medium_bound() {
     static const int v = [] {
         const char* e = getenv("PT_MEDIUM_BOUND");
@@ -1072,30 +1055,6 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     }
     lp.out.pass_rad = ctx->pass_rad;
     lp.out.via_rad = rad1 ? 1 : 0;
-    // path hand-over (DevOutput::spill): every lane of the pass launch hands over at most one path, so the
-    // records of one launch fit grid x PT_UBLOCK; the follow-up launch gets its own parameter block
-    const int K = pass_hand_supported(pc, pass_lds_bytes(ctx)) ? spill_threshold(ctx) : 0;
-    if (K > 0) {
-        const size_t cap = (size_t)grid * PT_UBLOCK;
-        if (cap > ctx->spill_cap) {
-            PT_HIP(hipStreamSynchronize(ctx->stream));  // an earlier launch may still use the old records
-            if (ctx->spill) (void)hipFree(ctx->spill);
-            ctx->spill = nullptr;
-            ctx->spill_cap = 0;
-            PT_HIP(hipMalloc(&ctx->spill, cap * 4 * sizeof(float4)));
-            ctx->spill_cap = cap;
-        }
-        if (!ctx->spill_count) PT_HIP(hipMalloc(&ctx->spill_count, sizeof(unsigned int)));
-        if (!ctx->params2) PT_HIP(hipMalloc(&ctx->params2, sizeof(LaunchParams)));
-        lp.out.spill = ctx->spill;
-        lp.out.spill_count = ctx->spill_count;
-        lp.out.spill_k = K;
-        lp.out.spill_consume = 0;
-        LaunchParams lc = lp;
-        lc.out.spill_k = 0;
-        lc.out.spill_consume = 1;
-        PT_HIP(hipMemcpyAsync(ctx->params2, &lc, sizeof(lc), hipMemcpyHostToDevice, ctx->stream));
-    }
     PT_HIP(hipMemcpyAsync(ctx->params, &lp, sizeof(lp), hipMemcpyHostToDevice, ctx->stream));
     for (int i = 0; i < pass_count;) {
         int b = 1, lg = 0;
@@ -1105,17 +1064,10 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         const int g = shared_grid(ctx, grid);
         const int w8 = write_u8 == 1 || (write_u8 == 2 && last);
         PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
-        if (K > 0) PT_HIP(hipMemsetAsync(ctx->spill_count, 0, sizeof(unsigned int), ctx->stream));
         int rc = ev_begin(ctx, 0);
         if (rc != PT_OK) return rc;
-        PT_HIP(launch_pass(ctx->params, pc, first, lg, w8, g, pass_lds_bytes(ctx), ctx->stream, K > 0 ? 1 : 0));
+        PT_HIP(launch_pass(ctx->params, pc, first, lg, w8, g, pass_lds_bytes(ctx), ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
-        if (K > 0) {  // the follow-up launch: the handed-over paths, densely packed, on a share of the grid
-            PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
-            if ((rc = ev_begin(ctx, 4)) != PT_OK) return rc;
-            PT_HIP(launch_pass(ctx->params2, pc, first, lg, w8, spill_grid(g), pass_lds_bytes(ctx), ctx->stream, 2));
-            if ((rc = ev_end(ctx)) != PT_OK) return rc;
-        }
         if (lg > 0 || rad1) {
             if (ctx->before_acc) {
                 const std::function<int()> f = std::move(ctx->before_acc);
@@ -1349,9 +1301,6 @@ extern "C" void pt_context_destroy(pt_context* ctx) {
     if (ctx->params) (void)hipFree(ctx->params);
     if (ctx->wave_mem) (void)hipFree(ctx->wave_mem);
     if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
-    if (ctx->spill) (void)hipFree(ctx->spill);
-    if (ctx->spill_count) (void)hipFree(ctx->spill_count);
-    if (ctx->params2) (void)hipFree(ctx->params2);
     for (int k = 0; k < 2; k++) {
         if (ctx->spec_rad[k]) (void)hipFree(ctx->spec_rad[k]);
         if (ctx->spec_params[k]) (void)hipFree(ctx->spec_params[k]);
@@ -1406,12 +1355,6 @@ extern "C" int pt_scene_info(pt_context* ctx, long long* bytes, int* node_num, i
     if (bytes) *bytes = (long long)ctx->scene_bytes;
     if (node_num) *node_num = ctx->node_num;
     if (triangle_num) *triangle_num = ctx->tri_num;
-    return PT_OK;
-}
-
-extern "C" int pt_set_spill(pt_context* ctx, int k) {
-    if (!ctx || k < -1 || k > 64) { set_error("bad spill threshold"); return PT_E_ARG; }
-    ctx->spill_k = k;
     return PT_OK;
 }
 

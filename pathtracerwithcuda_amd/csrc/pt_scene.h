@@ -149,14 +149,6 @@ struct DevOutput {
     float* pass_rad;         // batched passes: clamped radiance per (unit, pass) (12 B), summed in order
     int via_rad;             // 1: one-pass launches write pass_rad too (accumulate_kernel adds them afterwards)
     int pad;
-    // Path hand-over between a pass launch and its follow-up launch (pass_kernel_u, pt_set_spill): once the
-    // work is drained, a wave holding at most spill_k paths writes each of them, at its next segment start,
-    // as a 64-B record {o, medium} {d, depth} {thr, path seed} {rad, unit} to spill[] and ends; the follow-up
-    // launch (spill_consume = 1) takes the records as its units and carries the paths on, densely packed.
-    float4* spill;
-    unsigned int* spill_count;  // records written (zeroed before the pass launch)
-    int spill_k;                // > 0: hand over paths (the pass launch); 0: never
-    int spill_consume;          // 1: this launch's units are the records (the follow-up launch)
 };
 
 // Wavefront queues (pt_wavefront.hip). Ray slots are dense per depth; path state is per pixel.

@@ -104,11 +104,6 @@ class Renderer:
         (pt_set_medium_bound; None = the PT_MEDIUM_BOUND environment variable, the default: off)."""
         check(self._lib.pt_set_medium_bound(self._ctx, -1 if on is None else int(bool(on))), "pt_set_medium_bound")
 
-    def set_spill(self, k) -> None:
-        """Path hand-over (pt_set_spill): drained waves holding at most k paths hand them to a follow-up launch
-        (None = the PT_SPILL environment variable; 0 = off). Results do not depend on it."""
-        check(self._lib.pt_set_spill(self._ctx, -1 if k is None else int(k)), "pt_set_spill")
-
     def set_grid_share(self, percent: int) -> None:
         """Percentage of the occupancy-sized grid this context's pass launches take (frames in flight)."""
         check(self._lib.pt_set_grid_share(self._ctx, int(percent)), "pt_set_grid_share")

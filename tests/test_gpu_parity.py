@@ -468,48 +468,6 @@ def test_c5_4k_textured_depth12_frame(bench_gpu):
     assert launches == {0: 1, 3: 1}, launches
 
 
-@pytest.mark.parametrize("k", [16, 64])
-def test_path_hand_over_changes_nothing(bench_gpu, k):
-    """pt_set_spill: once a launch's work is drained, waves holding at most k paths hand them over
-    at their next segment start and a follow-up launch carries them on. The metric frame (8 passes in one
-    batch), rank 0's share of an 8-way tiling and the C4 medium scene are the same images bit for bit, and a
-    follow-up launch really ran (kind 4) and shaded paths (the segment count is the frame's)."""
-    import bench
-    r = bench_gpu
-    for wl_name, share in (("metric", 1), ("metric", 8), ("c3", 1)):
-        wl = bench.Workload(wl_name)
-        r.upload(wl.scene, wl.cfg)
-        r.setup_frame(wl.width, wl.height)
-        r.set_tiling(bench.BAND_ROWS, share, 0)
-        try:
-            r.set_spill(0)
-            r.stats_reset()
-            r.render(wl.cam, wl.cfg, 1, 8, write_u8=2)
-            r.synchronize()
-            want_seg = r.stats()["segments"]
-            full, full8 = r.download()
-            r.render(wl.cam, wl.cfg, 1, 1, write_u8=2)  # overwrite with a different frame
-            r.set_spill(k)
-            r.stats_reset()
-            r.render(wl.cam, wl.cfg, 1, 8, write_u8=2)
-            r.synchronize()
-            seg = r.stats()["segments"]
-            follow_ups = r.kernel_time_kind(4)[1]
-            img, img8 = r.download()
-        finally:
-            r.set_spill(None)
-            r.set_tiling(bench.BAND_ROWS, 1, 0)
-        assert follow_ups == 1 and seg == want_seg, (follow_ups, seg, want_seg)
-        assert np.array_equal(img.view(np.uint32), full.view(np.uint32)) and np.array_equal(img8, full8), wl_name
-    # the whole frame against the oracle through the hand-over, once
-    wl = bench.Workload("c2")
-    r.set_spill(k)
-    try:
-        _render_workload(r, wl, passes=8)
-    finally:
-        r.set_spill(None)
-
-
 def test_grid_share_changes_nothing_but_the_grid(bench_gpu):
     """pt_set_grid_share (half the grid per launch, bench.py with three frames in flight): rank 0's
     share of an 8-way tiled metric frame is the same image bit for bit."""
