@@ -1138,20 +1138,22 @@ int abi_render_pass(pt_context* ctx, const pt_render_camera* cam, const pt_confi
     if (slot >= 0) ctx->spec_served = true;
     if (slot < 0) {
         // A pass-1 miss right after a render-ahead that nobody used (the reference caller restarts at pass 1
-        // on every camera move: window.cpp:194-215, path_tracer.cpp:101-107) renders only its own pass: a
-        // moving camera then pays one one-pass launch per call instead of waiting for B/2 passes and leaving
-        // B/2 more queued ahead of its next call. A camera held still misses again at pass 2 and renders
-        // ahead from there.
-        const bool ahead = pass != 1 || ctx->spec_served;
+        // on every camera move: window.cpp:194-215, path_tracer.cpp:101-107) renders only its own pass, as the
+        // uncached path does (pass 1 overwrites: nothing to upload): a moving camera then pays one one-pass
+        // launch per call instead of waiting for B/2 passes and leaving B/2 more queued ahead of its next
+        // call. A camera held still misses again at pass 2 and renders ahead from there.
+        if (pass == 1 && !ctx->spec_served) {
+            ctx->spec_valid = false;
+            return render_passes(ctx, cam, config, pass, 1, 1);
+        }
         ctx->spec_served = false;
         int lg = 0;
-        while (ahead && (2 << lg) <= B / 2 && ((long long)units << (lg + 1)) <= (1ll << 28)) lg++;
+        while ((2 << lg) <= B / 2 && ((long long)units << (lg + 1)) <= (1ll << 28)) lg++;
         const int feat = render_feat(ctx, lp.cfg);
         const PassChoice pc = pass_choice(ctx, feat);
         ctx->last_kernel = pass_kernel_desc(pc, pass_lds_bytes(ctx));
         const size_t need = (size_t)units * ((size_t)1 << lg) * 12;
-        ctx->spec_first[1] = INT_MIN / 2;  // no second slot unless rendered below
-        for (int k = 0; k < (ahead ? 2 : 1); k++) {
+        for (int k = 0; k < 2; k++) {
             if (need > ctx->spec_rad_bytes[k]) {
                 PT_HIP(hipStreamSynchronize(ctx->stream));  // an earlier launch may still write the old buffer
                 if (ctx->spec_rad[k]) (void)hipFree(ctx->spec_rad[k]);
@@ -1162,7 +1164,7 @@ int abi_render_pass(pt_context* ctx, const pt_render_camera* cam, const pt_confi
             }
             LaunchParams ls = lp;
             ls.out.pass_rad = ctx->spec_rad[k];
-            ls.out.via_rad = lg == 0 ? 1 : 0;  // a one-pass slot too writes its radiance there, not into the image
+            ls.out.via_rad = lg == 0 ? 1 : 0;  // a one-pass slot (B = 2) too writes its radiance there
             const int first = pass + k * (1 << lg);
             PT_HIP(hipMemcpyAsync(ctx->spec_params[k], &ls, sizeof(ls), hipMemcpyHostToDevice, ctx->stream));
             PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));

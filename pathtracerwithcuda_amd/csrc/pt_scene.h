@@ -100,9 +100,11 @@ struct DevConfig {
     float air_n;
     float air_absorption[3];
     float air_reduced_scattering[3];
-    // length(v) > threshold tested as dot(v, v) > bound without the square root: bound is the largest
-    // float whose correctly rounded square root is <= the threshold (sqrtf is monotone), so both tests
-    // agree for every v, NaN included (pt_runtime.cpp sqrt_le_bound, tests/test_abi.py)
+    // length(v) > threshold tested as dot(v, v) > bound (and length(v) <= threshold as dot(v, v) <= bound)
+    // without the square root: bound is the largest float whose correctly rounded square root is <= the
+    // threshold (sqrtf is monotone), so each test agrees with its reference form for every v, NaN included
+    // (both are false for NaN; the kill test is therefore written !(dot <= bound), pt_path.h alive_after;
+    // pt_runtime.cpp sqrt_le_bound, tests/test_abi.py)
     float energy_len2;  // energy_exist_threshold (the kill test, path_tracer_kernel.cu:612-616)
     float sss_len2;     // sss_threshold (:460)
     float refr_len2;    // 0.000005f (fresnel.h:37, length(refraction) <= 0.000005f)

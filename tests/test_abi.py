@@ -85,8 +85,11 @@ def test_no_device_fails_loudly_without_gpu():
                                float("nan")])
 def test_sqrt_le_bound_replaces_length_tests_exactly(c):
     """pt_sqrt_le_bound(c) = the largest x >= 0 with sqrtf(x) <= c: the kernels test length(v) > c as
-    dot(v, v) > x. Checked at the boundary and on random squared lengths (numpy's float32 sqrt is the
-    correctly rounded sqrtf), NaN included."""
+    dot(v, v) > x (the SSS test, path_tracer_kernel.cu:460) and length(v) <= c as dot(v, v) <= x (the
+    Fresnel test, fresnel.h:37, and the kill test, :612-616, written !(dot <= x) for "alive": a NaN length
+    is not <= c, so a NaN throughput survives as in the reference). Both orderings are checked — each is
+    false for NaN, so neither is the other's negation there — at the boundary and on random squared
+    lengths (numpy's float32 sqrt is the correctly rounded sqrtf)."""
     lib = pt.lib()
     c32 = np.float32(c)
     x = np.float32(lib.pt_sqrt_le_bound(float(c32)))
@@ -106,3 +109,6 @@ def test_sqrt_le_bound_replaces_length_tests_exactly(c):
     with np.errstate(invalid="ignore"):
         assert np.array_equal(np.sqrt(d) > c32, d > x)
         assert np.array_equal(np.sqrt(d) <= c32, d <= x)
+        # the kernel's alive test (alive_after) against the reference's kill test, NaN included
+        assert np.array_equal(~(d <= x), ~(np.sqrt(d) <= c32))
+        assert (~(d <= x))[np.isnan(d)].all()
