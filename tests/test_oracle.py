@@ -184,6 +184,21 @@ def test_tolerance_to_a_cuda_like_build_c4(c4_subset, model):
     _assert_within_stated_tolerance(c4_subset, model)
 
 
+def test_medium_bound_walk_is_within_the_stated_tolerance(c4_subset):
+    """The medium-bounded walk (pt_set_medium_bound, a tolerance mode; pt_path.h medium_bound): in-medium
+    segments start every mesh walk with min_t = their free-flight distance (1 + 2^-10). On the C4 sample it
+    visits far fewer nodes and stays within the stated tolerance of the reference's unbounded walk (measured
+    on the whole C4 frame: identical, profiles/r04/medium_bound/oracle_study.txt)."""
+    wl, sel, a, sig_a = c4_subset
+    _, _, se = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, 8, pixels=sel)
+    b, _, sb = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, 8, pixels=sel, signatures=True, medium_bound=True)
+    assert sb["segments"] == se["segments"] and sb["nodes"] < 0.8 * se["nodes"]
+    d = np.abs(b.astype(np.float64) - a).max(axis=1)
+    flipped = (sig_a != sb["signatures"]).any(axis=0)
+    assert np.isfinite(b).all() and (d <= 1e-3).mean() >= 0.998 and flipped.mean() <= 0.03
+    assert ((d > 1e-3) & ~flipped).sum() <= 0.001 * len(sel)
+
+
 def test_cuda_intrinsic_model_errors_are_the_documented_maxima():
     """oracle_math.h OR_MATH_CUDA moves each intrinsic by the maximum error the CUDA C Programming Guide
     documents for it: __expf by 2 + floor(|1.173 x|) ulp, __logf by 2^-21.41 on [0.5, 2] (3 ulp elsewhere),
