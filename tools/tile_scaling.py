@@ -29,8 +29,14 @@ def main() -> None:
     ap.add_argument("--order", action="store_true", help="hand out bands most expensive first (pt_set_band_order)")
     ap.add_argument("--deal", type=int, default=1, help="with --order: deal the ranked bands over this many regions (8 = PT_SHARDS)")
     ap.add_argument("--band-rows", type=int, default=0, help="rows per band (default bench.BAND_ROWS)")
+    ap.add_argument("--spp", type=int, default=0,
+                    help="passes per rendered frame (default the workload's 8); ms figures are per 8 passes (one "
+                         "metric frame), so a 32-pass frame with PT_PASS_BATCH=32 tells what one launch for four "
+                         "frames would cost")
     args = ap.parse_args()
     wl = bench.Workload("metric")
+    spp = args.spp or wl.spp
+    scale = wl.spp / spp  # per-frame (8-pass) figures
     rs = []
     for _ in range(args.inflight):
         r = pt.Renderer(0)
@@ -48,15 +54,15 @@ def main() -> None:
                 q.set_tiling(args.band_rows or bench.BAND_ROWS, n, k)
                 if args.order:
                     q.order_bands_by_cost(wl.cam, wl.cfg, wl.spp, regions=args.deal)
-                q.render(wl.cam, wl.cfg, 1, wl.spp, write_u8=0)  # warm
+                q.render(wl.cam, wl.cfg, 1, spp, write_u8=0)  # warm
                 q.synchronize()
                 q.stats_reset()
             t0 = time.perf_counter()
             for f in range(args.frames):
-                rs[f % len(rs)].render(wl.cam, wl.cfg, 1, wl.spp, write_u8=0)
+                rs[f % len(rs)].render(wl.cam, wl.cfg, 1, spp, write_u8=0)
             for q in rs:
                 q.synchronize()
-            per_rank.append((time.perf_counter() - t0) / args.frames * 1e3)
+            per_rank.append((time.perf_counter() - t0) / args.frames * 1e3 * scale)
             kms, kn = r.kernel_time_kind(0)
             kern.append(kms / max(kn, 1))
         if base is None:
