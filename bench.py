@@ -283,6 +283,10 @@ def main() -> int:
     inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or (3 if world == 1 else 5)
     grid_share = int(os.environ.get("PT_BENCH_GRID_SHARE", "0")) or (
         (45 if inflight == 3 and not heavy else 100 // (inflight - 1)) if inflight >= 3 else 100)
+    # frames per launch (pt_render_frames, pathtracerwithcuda_amd.FrameGroup): each context renders G frames
+    # of the view in one pass launch and moves them with one collective, so a small share pays one launch's
+    # start and tail per G frames. Every frame is still rendered whole, with its own 8-bit output.
+    group = int(os.environ.get("PT_BENCH_GROUP", "0")) or 1
     wl = Workload(args.workload)
     scene, cfg, cam = wl.scene, wl.cfg, wl.cam
     width, height, spp = wl.width, wl.height, wl.spp
@@ -295,8 +299,12 @@ def main() -> int:
             q.set_medium_bound(True)
         q.upload(scene, cfg)
         rs.append(q)
-        frames.append(pt.TiledFrame(q, width, height, dist if world > 1 else None, BAND_ROWS,
-                                    device=f"cuda:{local}" if world > 1 else None))
+        if group > 1:
+            frames.append(pt.FrameGroup(q, width, height, group, dist if world > 1 else None, BAND_ROWS,
+                                        device=f"cuda:{local}"))
+        else:
+            frames.append(pt.TiledFrame(q, width, height, dist if world > 1 else None, BAND_ROWS,
+                                        device=f"cuda:{local}" if world > 1 else None))
     r = rs[0]
     schedule = r.schedule()
 
@@ -314,15 +322,20 @@ def main() -> int:
     last_full = int(os.environ.get("PT_BENCH_LAST_FULL", "1"))
 
     def run(k: int) -> None:
-        # the last frame of a batch has no frame behind it to fill the CUs its launch leaves: it takes
-        # the whole grid (every frame is still rendered completely, in order, on its own context)
+        # the last launch of a batch has no launch behind it to fill the CUs it leaves: it takes the whole
+        # grid (every frame is still rendered completely, in order, on its own context). With frame groups a
+        # launch takes the next min(G, frames left) frames.
         nonlocal nframe
-        for i in range(k):
+        launches = [min(group, k - i) for i in range(0, k, group)]
+        for j, n in enumerate(launches):
             q = frames[nframe % inflight]
-            full = grid_share < 100 and i >= k - last_full
+            full = grid_share < 100 and j >= len(launches) - last_full
             if full:
                 rs[nframe % inflight].set_grid_share(100)
-            q.launch(cam, cfg, spp)
+            if group > 1:
+                q.launch([cam] * n, cfg, spp)
+            else:
+                q.launch(cam, cfg, spp)
             if full:
                 rs[nframe % inflight].set_grid_share(grid_share)
             nframe += 1
@@ -366,7 +379,7 @@ def main() -> int:
     # image) with the frame its tiled context just gathered (the last frame of the latency loop above)
     matches_1gpu = None
     if world > 1 and rank == 0:
-        tiled, tiled8 = r.download()
+        tiled, tiled8 = frames[0].download()
         solo = pt.Renderer(local)
         try:
             if args.medium_bound:
@@ -397,7 +410,7 @@ def main() -> int:
 
     if args.save_image:
         from pathtracerwithcuda_amd.imageio import write_png
-        _, img8 = r.download()
+        _, img8 = frames[0].download()
         write_png(args.save_image, img8)
 
     value = segments / elapsed / 1e6
@@ -466,6 +479,7 @@ def main() -> int:
             "band_rows": BAND_ROWS if world > 1 else None,
             "ms_per_frame": round(ms_per_step, 3),
             "frames_in_flight": inflight,
+            "frames_per_launch": group,
             "hw_queues": int(hw_queues),
             "grid_share_pct": grid_share,
             "ms_per_frame_latency": round(latency * 1000.0, 3),

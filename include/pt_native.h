@@ -88,8 +88,20 @@ int pt_set_tiling(pt_context* ctx, int band_rows, int band_count, int band_index
  * Asynchronous on the context stream. */
 int pt_render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configuration* config,
                      int first_pass, int pass_count, int write_u8);
+/* Several frames at once: passes first_pass .. first_pass+pass_count-1 of `frames` frames, frame f seen
+ * through cams[f] (each of the frame's width) and summed into images[f] (width*height float3, device),
+ * its 8-bit output into images256[f] (device; images256 or an entry may be NULL: none). Frame f is
+ * bit-identical to pt_render_passes(cams[f]) on images[f]; the context's tiling applies to every frame.
+ * With the single-kernel schedule one launch per batch of passes renders all the frames, so they share
+ * one launch's start-up and tail; otherwise they render one after another. Asynchronous. */
+int pt_render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, const pt_configuration* config,
+                     int first_pass, int pass_count, int write_u8, float* const* images,
+                     unsigned char* const* images256);
 /* 8-bit gamma output of the current image for `pass` accumulated passes (after an external reduce). */
 int pt_finalize_u8(pt_context* ctx, const pt_configuration* config, int pass);
+/* The same for a caller's float image into a caller's 8-bit buffer (device; the frame's size). */
+int pt_finalize_u8_image(pt_context* ctx, const pt_configuration* config, int pass, const float* image,
+                         unsigned char* image256);
 int pt_synchronize(pt_context* ctx);
 /* The context's HIP stream (hipStream_t, non-blocking): callers order their own work on it (the
  * multi-GPU frame packs, gathers and finalizes on it, so frames in flight need no host sync). */

@@ -204,7 +204,10 @@ _PROTOS = {
     "pt_set_tiling": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
     "pt_render_passes": (C.c_int, [C.c_void_p, C.POINTER(RenderCamera), C.POINTER(Configuration), C.c_int, C.c_int,
                                    C.c_int]),
+    "pt_render_frames": (C.c_int, [C.c_void_p, C.POINTER(RenderCamera), C.c_int, C.POINTER(Configuration), C.c_int,
+                                   C.c_int, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     "pt_finalize_u8": (C.c_int, [C.c_void_p, C.POINTER(Configuration), C.c_int]),
+    "pt_finalize_u8_image": (C.c_int, [C.c_void_p, C.POINTER(Configuration), C.c_int, C.c_void_p, C.c_void_p]),
     "pt_synchronize": (C.c_int, [C.c_void_p]),
     "pt_stream_handle": (C.c_void_p, [C.c_void_p]),
     "pt_image_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),

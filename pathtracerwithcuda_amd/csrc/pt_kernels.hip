@@ -181,7 +181,8 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
 // (+2.5 % over starting survivors inside the shading batch, profiles/r02/onesite.txt). Every lane
 // still computes exactly the reference sequence for its path (same node order, same tests, same draws
 // keyed by (pass, pixel, depth)); only the interleaving between lanes changes.
-enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3, LANE_TRI = 4, LANE_NEW = 5 };
+// GEN: holding a unit whose camera path is not generated yet (a refill generates one frame's paths)
+enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3, LANE_TRI = 4, LANE_NEW = 5, LANE_GEN = 6 };
 
 // Starts the walk of the first mesh at or after `mesh` with a non-empty node range. The ranges of the
 // first PT_LDS_MESHES meshes come from the workgroup's LDS copy (lds_mesh, filled at kernel start), the
@@ -288,13 +289,20 @@ __device__ __forceinline__ bool next_root_mesh(const int2* lds_mesh, const float
 
 // pixel_256_transform_gamma_corrected_kernel (:644-680) for one finished (pixel, pass) unit
 // depth: the path's ray segments, counted into its band when the context measures band costs.
+__device__ __forceinline__ unsigned int frame_local(unsigned int u, unsigned int frame_units) {
+    while (u >= frame_units) u -= frame_units;
+    return u;
+}
+
+// unit: the launch's unit (pass_rad index); lu: its unit within its frame copy (pt_render_frames; lu == unit for
+// one copy)
 __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfig& cfg, const DevOutput& out,
-                                            const PathState& ps, unsigned int unit, int first_pass, int write_u8,
-                                            int batch_log2, float clamp_hi, int depth) {
-    if (til.band_cost) atomicAdd(&til.band_cost[pixel_band(til, unit_to_pixel(til, unit >> batch_log2))], (unsigned int)depth);
+                                            const PathState& ps, unsigned int unit, unsigned int lu, int first_pass,
+                                            int write_u8, int batch_log2, float clamp_hi, int depth) {
+    if (til.band_cost) atomicAdd(&til.band_cost[pixel_band(til, unit_to_pixel(til, lu >> batch_log2))], (unsigned int)depth);
     const v3 c = clamp3(ps.rad, 0.0f, clamp_hi);
-    if (batch_log2 == 0 && !out.via_rad) {
-        const int pixel = unit_to_pixel(til, unit);
+    if (batch_log2 == 0 && !out.via_rad) {  // (never for several frame copies: they go through pass_rad)
+        const int pixel = unit_to_pixel(til, lu);
         float* img = out.image + (size_t)pixel * 3;
         v3 sum;
         if (first_pass != 1) sum = mk3(img[0], img[1], img[2]) + c;
@@ -368,7 +376,9 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     float wbound = __builtin_inff();  // every mesh walk's starting min_t (medium-bounded mode only)
     unsigned long long segments = 0;  // wave-uniform: lanes shaded (ray segments traced)
     Counters none = {0u, 0u, 0u, 0u, 0u, 0u};
-    const unsigned int units = (unsigned int)P0->til.unit_count << batch_log2;
+    // the units of one frame copy; a pt_render_frames launch has `frames` copies one after another
+    const unsigned int frame_units = (unsigned int)P0->til.unit_count << batch_log2;
+    const unsigned int units = frame_units * (unsigned int)max(1, P0->out.frames);
     const EvenRegions regions{units, (units + PT_SHARDS - 1) / PT_SHARDS};
     WorkCursor cursor = work_begin();
     bool drained = false;
@@ -413,25 +423,41 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (want) {
                 if (u != ~0u) {
                     unit = u;
-                    const int pixel = unit_to_pixel(til, u >> batch_log2);
-                    const int32_t hseed = hash_pt(first_pass + (int)(u & ((1u << batch_log2) - 1u)));
-                    const DevCamera cam = load_const(&P->cam);
-                    if (PT_DUP == 4) {
-                        PathState p2; int px2 = pixel, hs2 = hseed;
-                        opaque(px2); opaque(hs2);
-                        generate_path(cam, cfg, px2, hs2, &p2);
-                        opaque(p2);
-                    }
-                    generate_path(cam, cfg, pixel, hseed, &ps);
-                    pseed = path_seed(hseed, pixel);
-                    depth = 0;
-                    if (cfg.max_depth > 0) {
-                        mode = LANE_NEW;
-                    } else {
-                        finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
-                    }
+                    mode = LANE_GEN;
                 } else if (drained) {
                     mode = LANE_DONE;
+                }
+            }
+        }
+        // lanes holding a new unit start its camera path. The camera is read through the scalar cache, so one
+        // refill starts the paths of one frame (pt_render_frames): those of the first such lane's frame; a lane
+        // whose unit lies in another frame (a refill that spans two frames' units) starts in the next round
+        const unsigned long long gen_mask = __ballot(mode == LANE_GEN);
+        if (gen_mask) {
+            unsigned int lu = unit;  // the unit within its frame
+            int frame = 0;
+            if (mode == LANE_GEN) {
+                while (lu >= frame_units) { lu -= frame_units; frame++; }
+            }
+            const int f0 = __builtin_amdgcn_readlane(frame, (int)__builtin_ctzll(gen_mask));
+            if (mode == LANE_GEN && frame == f0) {
+                const int pixel = unit_to_pixel(til, lu >> batch_log2);
+                const int32_t hseed = hash_pt(first_pass + (int)(lu & ((1u << batch_log2) - 1u)));
+                const DevCamera cam = load_const((out.frames > 1 ? out.cams : &P->cam) + f0);
+                if (PT_DUP == 4) {
+                    PathState p2; int px2 = pixel, hs2 = hseed;
+                    opaque(px2); opaque(hs2);
+                    generate_path(cam, cfg, px2, hs2, &p2);
+                    opaque(p2);
+                }
+                generate_path(cam, cfg, pixel, hseed, &ps);
+                pseed = path_seed(hseed, pixel);
+                depth = 0;
+                if (cfg.max_depth > 0) {
+                    mode = LANE_NEW;
+                } else {
+                    finish_unit(til, cfg, out, ps, unit, lu, first_pass, write_u8, batch_log2, clamp_hi, depth);
+                    mode = LANE_WANT;
                 }
             }
         }
@@ -467,7 +493,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (mode == LANE_READY) {  // the pass's end for this unit, or the next trace step
                 depth++;
                 if (!alive || depth >= cfg.max_depth) {
-                    finish_unit(til, cfg, out, ps, unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
+                    finish_unit(til, cfg, out, ps, unit, frame_local(unit, frame_units), first_pass, write_u8, batch_log2, clamp_hi, depth);
                     mode = LANE_WANT;
                 } else {
                     mode = LANE_NEW;  // its next segment starts in the next round's refill, with the new paths
@@ -575,14 +601,17 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
 
 // The running sum over a batch of passes, in pass order (path_tracer_kernel.cu:644-651 applied
 // pass after pass), then the 8-bit output of the batch's last pass.
+// frame: which frame copy of a pt_render_frames launch (0 otherwise)
+// frame's running sum `image` and 8-bit output `image256` (the launch's own, or a pt_render_frames frame's)
 __global__ __launch_bounds__(PT_BLOCK) void accumulate_kernel(const LaunchParams* __restrict__ P, int first_pass,
-                                                              int batch_log2, int write_u8) {
+                                                              int batch_log2, int write_u8, int frame,
+                                                              float* __restrict__ image, uint8_t* __restrict__ image256) {
     const unsigned int lu = blockIdx.x * PT_BLOCK + threadIdx.x;
     if (lu >= (unsigned int)P->til.unit_count) return;
     const int pixel = unit_to_pixel(P->til, lu);
     const int batch = 1 << batch_log2;
-    float* img = P->out.image + (size_t)pixel * 3;
-    const float* pr = P->out.pass_rad + ((size_t)lu << batch_log2) * 3;
+    float* img = image + (size_t)pixel * 3;
+    const float* pr = P->out.pass_rad + (((size_t)frame * (size_t)P->til.unit_count + lu) << batch_log2) * 3;
     v3 sum = first_pass == 1 ? mk3(0.0f, 0.0f, 0.0f) : mk3(img[0], img[1], img[2]);  // pass 1 overwrites
     if ((batch & 3) == 0) {  // four passes = 12 floats = three 16-B loads (the unit's run is 16-B aligned)
         const float4* q = reinterpret_cast<const float4*>(pr);
@@ -599,8 +628,7 @@ __global__ __launch_bounds__(PT_BLOCK) void accumulate_kernel(const LaunchParams
         }
     }
     img[0] = sum.x; img[1] = sum.y; img[2] = sum.z;
-    if (write_u8 && P->out.image256)
-        store_u8(P->cfg, sum, first_pass + batch - 1, P->out.image256 + (size_t)pixel * 3);
+    if (write_u8 && image256) store_u8(P->cfg, sum, first_pass + batch - 1, image256 + (size_t)pixel * 3);
 }
 
 // One pass of a batched launch added into the running sum: pass `pass` is slot j of every unit's run of
@@ -965,10 +993,10 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
 }
 
 hipError_t launch_accumulate(const LaunchParams* params_dev, int units, int first_pass, int batch_log2, int write_u8,
-                             hipStream_t stream) {
+                             hipStream_t stream, int frame, float* image, uint8_t* image256) {
     if (units <= 0) return hipSuccess;
     hipLaunchKernelGGL(accumulate_kernel, dim3((units + PT_BLOCK - 1) / PT_BLOCK), dim3(PT_BLOCK), 0, stream,
-                       params_dev, first_pass, batch_log2, write_u8);
+                       params_dev, first_pass, batch_log2, write_u8, frame, image, image256);
     return hipGetLastError();
 }
 

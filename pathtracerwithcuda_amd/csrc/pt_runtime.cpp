@@ -504,6 +504,9 @@ struct pt_context {
     // batched passes of the single-kernel schedule: clamped radiance per (unit, pass)
     float* pass_rad = nullptr;
     size_t pass_rad_bytes = 0;
+    // pt_render_frames: the frames' cameras (device)
+    DevCamera* cams = nullptr;
+    int cams_cap = 0;
     // thread_shrink scratch
     int* shrink_buf = nullptr;
     int* shrink_tiles = nullptr;
@@ -1079,9 +1082,87 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
                 ctx->acc_wait = nullptr;
             }
             if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;
-            PT_HIP(launch_accumulate(ctx->params, units, first, lg, w8, ctx->stream));
+            PT_HIP(launch_accumulate(ctx->params, units, first, lg, w8, ctx->stream, 0, ctx->image, ctx->image256));
             if ((rc = ev_end(ctx)) != PT_OK) return rc;
         }
+        i += b;
+    }
+    return PT_OK;
+}
+
+// pt_render_frames: `frames` frames of the same passes, frame f through cams[f] into images[f] (and
+// images256[f]). With pass_kernel_u, one launch per batch of passes takes every frame's units (frame f's
+// are f * units_per_frame + its units), so the frames share one launch's start and tail instead of each
+// paying its own; its accumulate launches then sum each frame's pass radiances into that frame's image.
+// Otherwise (the wavefront schedule, pass_kernel) the frames render one after another on the context.
+// Either way frame f is bit-identical to pt_render_passes of cams[f] on images[f].
+int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, const pt_configuration* config,
+                  int first_pass, int pass_count, int write_u8, float* const* images, uint8_t* const* images256) {
+    LaunchParams lp;
+    int prc = prepare_launch(ctx, cams, config, lp);
+    if (prc != PT_OK) return prc;
+    for (int f = 1; f < frames; f++)
+        if ((int)cams[f].resolution.x != ctx->width) { set_error("camera width != frame width"); return PT_E_ARG; }
+    const int feat = render_feat(ctx, lp.cfg);
+    const PassChoice pc = pass_choice(ctx, feat);
+    const bool fused = frames > 1 && !wavefront_schedule(ctx) && pass_uses_unified(pc, pass_lds_bytes(ctx));
+    if (!fused) {
+        float* const img0 = ctx->image;
+        uint8_t* const img8 = ctx->image256;
+        int rc = PT_OK;
+        for (int f = 0; f < frames && rc == PT_OK; f++) {
+            ctx->image = images[f];
+            ctx->image256 = images256 ? images256[f] : nullptr;
+            rc = render_passes(ctx, cams + f, config, first_pass, pass_count, write_u8);
+        }
+        ctx->image = img0;
+        ctx->image256 = img8;
+        return rc;
+    }
+    const int units = ctx->tiling.unit_count;
+    if ((long long)units * frames > (1ll << 28)) { set_error("too many frames for one launch"); return PT_E_ARG; }
+    if (ctx->cams_cap < frames) {
+        if (ctx->cams) (void)hipFree(ctx->cams);
+        ctx->cams = nullptr;
+        ctx->cams_cap = 0;
+        PT_HIP(hipMalloc(&ctx->cams, (size_t)frames * sizeof(DevCamera)));
+        ctx->cams_cap = frames;
+    }
+    std::vector<DevCamera> dc((size_t)frames);
+    for (int f = 0; f < frames; f++) dc[(size_t)f] = to_dev(cams[f]);
+    PT_HIP(hipMemcpyAsync(ctx->cams, dc.data(), dc.size() * sizeof(DevCamera), hipMemcpyHostToDevice, ctx->stream));
+    const int grid = pass_grid(ctx, feat);
+    ctx->last_kernel = pass_kernel_desc(pc, pass_lds_bytes(ctx));
+    int most = 1;
+    while (most * 2 <= max_pass_batch() && (long long)units * most * 2 * frames <= (1ll << 28)) most *= 2;
+    const size_t need = (size_t)units * (size_t)most * (size_t)frames * 12;
+    if (need > ctx->pass_rad_bytes) {
+        if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
+        ctx->pass_rad = nullptr;
+        ctx->pass_rad_bytes = 0;
+        PT_HIP(hipMalloc(&ctx->pass_rad, need));
+        ctx->pass_rad_bytes = need;
+    }
+    lp.out.pass_rad = ctx->pass_rad;
+    lp.out.via_rad = 1;  // every frame's radiances go through pass_rad, one-pass launches included
+    lp.out.frames = frames;
+    lp.out.cams = ctx->cams;
+    PT_HIP(hipMemcpyAsync(ctx->params, &lp, sizeof(lp), hipMemcpyHostToDevice, ctx->stream));
+    for (int i = 0; i < pass_count;) {
+        int b = 1, lg = 0;
+        while (b * 2 <= most && i + b * 2 <= pass_count) { b *= 2; lg++; }
+        const int first = first_pass + i;
+        const int w8 = write_u8 == 1 || (write_u8 == 2 && i + b == pass_count);
+        PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
+        int rc = ev_begin(ctx, 0);
+        if (rc != PT_OK) return rc;
+        PT_HIP(launch_pass(ctx->params, pc, first, lg, w8, shared_grid(ctx, grid), pass_lds_bytes(ctx), ctx->stream));
+        if ((rc = ev_end(ctx)) != PT_OK) return rc;
+        if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;
+        for (int f = 0; f < frames; f++)
+            PT_HIP(launch_accumulate(ctx->params, units, first, lg, w8, ctx->stream, f, images[f],
+                                     images256 ? images256[f] : nullptr));
+        if ((rc = ev_end(ctx)) != PT_OK) return rc;
         i += b;
     }
     return PT_OK;
@@ -1303,6 +1384,7 @@ extern "C" void pt_context_destroy(pt_context* ctx) {
     if (ctx->params) (void)hipFree(ctx->params);
     if (ctx->wave_mem) (void)hipFree(ctx->wave_mem);
     if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
+    if (ctx->cams) (void)hipFree(ctx->cams);
     for (int k = 0; k < 2; k++) {
         if (ctx->spec_rad[k]) (void)hipFree(ctx->spec_rad[k]);
         if (ctx->spec_params[k]) (void)hipFree(ctx->spec_params[k]);
@@ -1542,6 +1624,27 @@ extern "C" int pt_render_passes(pt_context* ctx, const pt_render_camera* cam, co
     int rc = ensure_device(ctx);
     if (rc != PT_OK) return rc;
     return render_passes(ctx, cam, config, first_pass, pass_count, write_u8);
+}
+
+extern "C" int pt_render_frames(pt_context* ctx, const pt_render_camera* cams, int frames,
+                                const pt_configuration* config, int first_pass, int pass_count, int write_u8,
+                                float* const* images, unsigned char* const* images256) {
+    if (!ctx || first_pass < 1 || pass_count < 0) { set_error("bad pass range"); return PT_E_ARG; }
+    if (!cams || !images || frames < 1) { set_error("null cameras/images or no frames"); return PT_E_ARG; }
+    for (int f = 0; f < frames; f++)
+        if (!images[f]) { set_error("null frame image"); return PT_E_ARG; }
+    int rc = ensure_device(ctx);
+    if (rc != PT_OK) return rc;
+    return render_frames(ctx, cams, frames, config, first_pass, pass_count, write_u8, images, images256);
+}
+
+extern "C" int pt_finalize_u8_image(pt_context* ctx, const pt_configuration* config, int pass, const float* image,
+                                    unsigned char* image256) {
+    if (!ctx || !config || pass < 1 || !image || !image256) return PT_E_ARG;
+    int rc = ensure_device(ctx);
+    if (rc != PT_OK) return rc;
+    PT_HIP(launch_u8(to_dev(*config), image, image256, ctx->width * ctx->height, pass, ctx->stream));
+    return PT_OK;
 }
 
 extern "C" int pt_finalize_u8(pt_context* ctx, const pt_configuration* config, int pass) {

@@ -150,7 +150,11 @@ struct DevOutput {
     unsigned long long* stats;  // [0] ray segments, [1..] optional instrumentation
     float* pass_rad;         // batched passes: clamped radiance per (unit, pass) (12 B), summed in order
     int via_rad;             // 1: one-pass launches write pass_rad too (accumulate_kernel adds them afterwards)
-    int pad;
+    // pt_render_frames: one pass_kernel_u launch renders `frames` frames of the batch (>= 1; 1 otherwise), frame
+    // f seen through cams[f]: its units are f * (unit_count << batch_log2) + the unit, its radiances the same
+    // range of pass_rad (always via pass_rad), summed into its own image by accumulate_kernel
+    int frames;
+    const DevCamera* cams;   // frames > 1 only (the launch's `cam` otherwise)
 };
 
 // Wavefront queues (pt_wavefront.hip). Ray slots are dense per depth; path state is per pixel.

@@ -42,6 +42,13 @@ def camera(width: int, height: int, fov: float = 45.0, yaw: float = 0.0, pitch: 
     return rc
 
 
+def _device_ptr(x) -> int | None:
+    """A device buffer as an address: an int, or a tensor's data_ptr() (None / 0 stay null)."""
+    if x is None:
+        return None
+    return int(x.data_ptr()) if hasattr(x, "data_ptr") else int(x)
+
+
 def deal_bands(ranked: list[int], n: int, regions: int) -> list[int]:
     """Band order for `n` local bands (positions n - len(ranked) .. n - 1 beyond the ranked ones keep
     their band: the partial last band) whose units a launch cuts into `regions` equal contiguous
@@ -176,8 +183,27 @@ class Renderer:
         check(self._lib.pt_render_passes(self._ctx, C.byref(cam), C.byref(config), first_pass, pass_count, write_u8),
               "pt_render_passes")
 
+    def render_frames(self, cams, config: Configuration, images, images256=None, first_pass: int = 1,
+                      pass_count: int = 1, write_u8: int = 2) -> None:
+        """pt_render_frames: the same passes of len(cams) frames, frame f through cams[f] into the device buffers
+        images[f] (width*height float3) and images256[f] (uchar3, optional): one pass launch per batch of
+        passes for all of them. Buffers are device pointers (int) or CUDA tensors."""
+        n = len(cams)
+        if len(images) != n or (images256 is not None and len(images256) != n):
+            raise ValueError("one image (and 8-bit image) per camera")
+        arr = (RenderCamera * n)(*cams)
+        imgs = (C.c_void_p * n)(*[_device_ptr(x) for x in images])
+        imgs8 = (C.c_void_p * n)(*[_device_ptr(x) for x in images256]) if images256 is not None else None
+        check(self._lib.pt_render_frames(self._ctx, arr, n, C.byref(config), first_pass, pass_count, write_u8, imgs,
+                                         imgs8), "pt_render_frames")
+
     def finalize_u8(self, config: Configuration, passes: int) -> None:
         check(self._lib.pt_finalize_u8(self._ctx, C.byref(config), passes), "pt_finalize_u8")
+
+    def finalize_u8_image(self, config: Configuration, passes: int, image, image256) -> None:
+        """8-bit gamma output of a caller's float image (device pointer or CUDA tensor) into image256."""
+        check(self._lib.pt_finalize_u8_image(self._ctx, C.byref(config), passes, _device_ptr(image),
+                                             _device_ptr(image256)), "pt_finalize_u8_image")
 
     def synchronize(self) -> None:
         check(self._lib.pt_synchronize(self._ctx), "pt_synchronize")

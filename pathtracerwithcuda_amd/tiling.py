@@ -131,3 +131,112 @@ class TiledFrame:
         """Passes 1..spp; rank 0 ends with the full float image and its 8-bit output."""
         self.launch(cam, cfg, spp)
         self.synchronize()
+
+    def download(self):
+        """Rank 0's frame after a render: the float running sum and the 8-bit image (numpy)."""
+        return self.r.download()
+
+
+class FrameGroup:
+    """`frames` frames per launch on this rank's bands (pt_render_frames), then ONE collective for all of
+    them: the group's float images are one [frames, height * width * 3] buffer, so the gather moves every
+    frame's rows in one call (the reduce sums the whole stack). The frames share one pass launch's start
+    and tail instead of each paying its own, which is most of a small share's cost. Frame f
+    of a launch is bit-identical to a TiledFrame's frame through the same camera.
+
+    The renderer additionally needs render_frames and finalize_u8_image (the Renderer interface)."""
+
+    def __init__(self, renderer, width: int, height: int, frames: int, dist=None, band_rows: int = 8,
+                 device=None, collective: str | None = None):
+        import torch
+
+        self.r = renderer
+        self.width, self.height, self.frames = width, height, frames
+        self.dist = dist if (dist is not None and dist.is_available() and dist.is_initialized()) else None
+        self.world = self.dist.get_world_size() if self.dist else 1
+        self.rank = self.dist.get_rank() if self.dist else 0
+        self.band_rows = band_rows
+        self.collective = collective or os.environ.get("PT_FRAME_COLLECTIVE", "gather")
+        if self.collective not in ("gather", "reduce"):
+            raise ValueError(f"unknown frame collective {self.collective!r}")
+        device = device or "cuda:0"
+        n = width * height * 3
+        self.stack = torch.zeros(frames, n, dtype=torch.float32, device=device)
+        self.stack8 = torch.zeros(frames, n, dtype=torch.uint8, device=device)
+        self.images = list(self.stack.unbind(0))
+        self.images8 = list(self.stack8.unbind(0))
+        renderer.setup_frame(width, height, self.images[0].data_ptr())  # the frame geometry
+        self.stream = None
+        self.last = 0  # frames of the last launch
+        if self.world > 1:
+            renderer.set_tiling(band_rows, self.world, self.rank)
+            self.rows = [torch.as_tensor(owned_rows(height, band_rows, self.world, k), device=device)
+                         for k in range(self.world)]
+            most = max(len(rw) for rw in self.rows)
+            self.most = most
+            self.part = torch.zeros(frames, most, width, 3, dtype=torch.float32, device=device)
+            self.parts = None
+            if self.rank == 0:
+                self.landing = torch.zeros(self.world, frames, most, width, 3, dtype=torch.float32, device=device)
+                self.parts = list(self.landing.unbind(0))
+                src = [k * most + torch.arange(len(self.rows[k]), device=device) for k in range(1, self.world)]
+                self.src_rows = torch.cat(src)
+                self.dst_rows = torch.cat([self.rows[k] for k in range(1, self.world)])
+        if self.stack.is_cuda and hasattr(renderer, "stream_handle"):
+            self.stream = torch.cuda.ExternalStream(renderer.stream_handle(), device=self.stack.device)
+
+    def _on_stream(self):
+        import contextlib
+
+        if self.stream is None:
+            return contextlib.nullcontext()
+        import torch
+
+        return torch.cuda.stream(self.stream)
+
+    def launch(self, cams, cfg, spp: int) -> None:
+        """Queues passes 1..spp of len(cams) <= frames frames (frame f through cams[f]), then (world > 1) the
+        group's one collective and rank 0's 8-bit outputs, in order on the renderer's stream."""
+        n = len(cams)
+        if not 1 <= n <= self.frames:
+            raise ValueError(f"1..{self.frames} cameras per launch, got {n}")
+        self.last = n
+        if self.world == 1:
+            with self._on_stream():
+                self.r.render_frames(list(cams), cfg, self.images[:n], self.images8[:n], 1, spp, write_u8=2)
+            return
+        with self._on_stream():
+            if self.collective == "reduce":
+                self.stack[:n].zero_()  # rows outside this rank's bands must be zero for the reduce
+            self.r.render_frames(list(cams), cfg, self.images[:n], None, 1, spp, write_u8=0)
+            if self.stream is None:
+                self.r.synchronize()
+            if self.collective == "reduce":
+                self.dist.reduce(self.stack, dst=0)  # the one collective of the group
+            else:
+                img = self.stack.view(self.frames, self.height, self.width, 3)
+                mine = self.rows[self.rank]
+                self.part[:n, :len(mine)] = img[:n, mine]
+                self.dist.gather(self.part, gather_list=self.parts, dst=0)  # the one collective of the group
+                if self.rank == 0:
+                    land = self.landing.transpose(0, 1).reshape(self.frames, self.world * self.most, self.width, 3)
+                    img[:n, self.dst_rows] = land[:n, self.src_rows]
+            if self.rank == 0:
+                for f in range(n):
+                    self.r.finalize_u8_image(cfg, spp, self.images[f], self.images8[f])
+
+    def synchronize(self) -> None:
+        self.r.synchronize()
+        if self.stream is not None:
+            self.stream.synchronize()
+
+    def render(self, cam, cfg, spp: int) -> None:
+        """One frame (frame 0 of the group); rank 0 ends with its float image and 8-bit output."""
+        self.launch([cam], cfg, spp)
+        self.synchronize()
+
+    def download(self, frame: int = 0):
+        """Frame `frame` of the last launch as (float image, 8-bit image), numpy [height, width, 3]."""
+        shape = (self.height, self.width, 3)
+        return (self.stack[frame].cpu().numpy().reshape(shape).copy(),
+                self.stack8[frame].cpu().numpy().reshape(shape).copy())

@@ -4,7 +4,10 @@ INFLIGHT frames in flight, each launch on 1 / (INFLIGHT - 1) of the grid from th
 frame on the whole grid, rank 0 collecting the frame) on the HIP renderer. Rank 0 saves each
 context's float image and 8-bit image for the test to compare with the oracle.
 
-    worker.py OUT_PREFIX COLLECTIVE FRAMES [INFLIGHT]
+With GROUP > 1 every context is a FrameGroup: each launch renders GROUP frames, frame j through the camera
+turned by yaw 0.3 j (GROUP cameras), moved by one collective; rank 0 saves every frame of every context.
+
+    worker.py OUT_PREFIX COLLECTIVE LAUNCHES [INFLIGHT [GROUP]]
 """
 import os
 import sys
@@ -26,6 +29,7 @@ def scene():
 def main() -> int:
     out, collective, frames = sys.argv[1], sys.argv[2], int(sys.argv[3])
     inflight = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+    group = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     share = 100 // (inflight - 1) if inflight >= 3 else 100
     import torch.distributed as dist
 
@@ -42,19 +46,29 @@ def main() -> int:
         r.set_grid_share(share)
         r.upload(sc, cfg)
         rs.append(r)
-        fr.append(pt.TiledFrame(r, W, H, dist, 8, device="cuda:0", collective=collective))
+        if group > 1:
+            fr.append(pt.FrameGroup(r, W, H, group, dist, 8, device="cuda:0", collective=collective))
+        else:
+            fr.append(pt.TiledFrame(r, W, H, dist, 8, device="cuda:0", collective=collective))
+    cams = [pt.camera(W, H, yaw=0.3 * j, **CAM) for j in range(group)]
     for i in range(frames):
         last = i == frames - 1 and share < 100
         if last:
             rs[i % inflight].set_grid_share(100)
-        fr[i % inflight].launch(cam, cfg, SPP)
+        fr[i % inflight].launch(cams if group > 1 else cam, cfg, SPP)
     for f in fr:
         f.synchronize()
     if rank == 0:
         for k, (r, f) in enumerate(zip(rs, fr)):
-            _, img8 = r.download()
-            np.save(f"{out}_{k}_f.npy", f.image.cpu().numpy().reshape(-1, 3))
-            np.save(f"{out}_{k}_u8.npy", img8.reshape(-1, 3))
+            if group > 1:
+                for j in range(group):
+                    img, img8 = f.download(j)
+                    np.save(f"{out}_{k}_{j}_f.npy", img.reshape(-1, 3))
+                    np.save(f"{out}_{k}_{j}_u8.npy", img8.reshape(-1, 3))
+            else:
+                _, img8 = r.download()
+                np.save(f"{out}_{k}_f.npy", f.image.cpu().numpy().reshape(-1, 3))
+                np.save(f"{out}_{k}_u8.npy", img8.reshape(-1, 3))
     dist.barrier()
     for r in rs:
         r.close()

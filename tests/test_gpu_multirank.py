@@ -44,3 +44,27 @@ def test_tiled_frames_on_hip_equal_the_oracle(require_gpu, tmp_path, ranks, coll
         img8 = np.load(f"{out}_{k}_u8.npy")
         assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), f"context {k}: float image"
         assert np.array_equal(img8, ref8), f"context {k}: 8-bit image"
+
+
+@pytest.mark.parametrize("ranks,collective,inflight,group", [(2, "gather", 3, 4), (3, "reduce", 2, 3)])
+def test_frame_groups_on_hip_equal_the_oracle(require_gpu, tmp_path, ranks, collective, inflight, group):
+    """bench.py's PT_BENCH_GROUP path: FrameGroup contexts (pt_render_frames, one collective per group) with
+    frames in flight; every frame of every context equals the oracle's frame of its camera."""
+    out = str(tmp_path / "mg")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(HERE, "gpu_multirank_worker.py"), out, collective, str(2 * inflight + 1), str(inflight),
+           str(group)]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert res.returncode == 0, res.stderr[-4000:]
+    sc = worker.scene()
+    cfg = pt.configuration(max_tracer_depth=8)
+    for j in range(group):
+        cam = pt.camera(worker.W, worker.H, yaw=0.3 * j, **worker.CAM)
+        ref, ref8, _ = oracle.render(sc.view, cam, cfg, 1, worker.SPP)
+        for k in range(inflight):
+            img = np.load(f"{out}_{k}_{j}_f.npy")
+            img8 = np.load(f"{out}_{k}_{j}_u8.npy")
+            assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), f"context {k} frame {j}: float"
+            assert np.array_equal(img8, ref8), f"context {k} frame {j}: 8-bit"

@@ -638,6 +638,49 @@ def test_edge_cases(gpu, case):
     assert_bitwise(img8.reshape(-1, 3), ref8, f"{case} 8-bit")
 
 
+@pytest.mark.parametrize("case", ["one_launch", "odd_range", "tiled", "grid_share"])
+def test_render_frames_equal_separate_frames(gpu, case):
+    """pt_render_frames: several frames, each through its own camera, in one pass launch per batch of passes
+    (the persistent schedule; the wavefront schedule renders them one after another). Every frame is the
+    oracle's frame of its camera bit for bit, 8-bit output included: a refill whose units span two frames
+    generates one frame's paths and the other frame's in the next round, and frame f's radiances are summed
+    into its own image. Cases: one 8-pass launch; a continuation range 2..4 (batches of 2 and 1, the
+    one-pass launch through pass_rad too); a 3-band share (rows of band 1 only); a 45 % grid."""
+    import torch
+
+    sc = pt.cornell_scene(pt.torus_knot(60, 16), cube_length=32)
+    cfg = pt.configuration(max_tracer_depth=6)
+    W, H = 72, 48
+    cams = [pt.camera(W, H, yaw=y, **BENCH_CAM) for y in (0.0, 0.4, -0.7)]
+    first, count = (2, 3) if case == "odd_range" else (1, 8)
+    gpu.upload(sc, cfg)
+    gpu.setup_frame(W, H)
+    if case == "tiled":
+        gpu.set_tiling(8, 3, 1)
+    if case == "grid_share":
+        gpu.set_grid_share(45)
+    try:
+        imgs = [torch.full((H * W * 3,), 7.0, dtype=torch.float32, device="cuda:0") for _ in cams]
+        imgs8 = [torch.zeros((H * W * 3,), dtype=torch.uint8, device="cuda:0") for _ in cams]
+        if first > 1:
+            gpu.render_frames(cams, cfg, imgs, imgs8, 1, first - 1, write_u8=0)
+        gpu.render_frames(cams, cfg, imgs, imgs8, first, count, write_u8=2)
+        gpu.synchronize()
+        rows = [y for y in range(H) if (y // 8) % 3 == 1] if case == "tiled" else list(range(H))
+        for f, cam in enumerate(cams):
+            ref, ref8, _ = oracle.render(sc.view, cam, cfg, 1, first - 1 + count)
+            img = imgs[f].cpu().numpy().reshape(H, W, 3)[rows]
+            img8 = imgs8[f].cpu().numpy().reshape(H, W, 3)[rows]
+            assert_bitwise(img.reshape(-1, 3), ref.reshape(H, W, 3)[rows].reshape(-1, 3), f"{case} frame {f} float")
+            assert_bitwise(img8.reshape(-1, 3), ref8.reshape(H, W, 3)[rows].reshape(-1, 3), f"{case} frame {f} 8-bit")
+            if case == "tiled":  # rows outside the share untouched
+                other = [y for y in range(H) if y not in rows]
+                assert (imgs[f].cpu().numpy().reshape(H, W, 3)[other] == 7.0).all()
+    finally:
+        gpu.set_tiling(1, 1, 0)
+        gpu.set_grid_share(100)
+
+
 @pytest.mark.parametrize("inflight", [2, 3, 5])
 def test_frames_in_flight_equal_one_at_a_time(require_gpu, inflight):
     """bench.py's frame pipeline: frames queued on several contexts with no host sync between them

@@ -48,11 +48,23 @@ class OracleFrameRenderer:
         if write_u8:
             self.img8[px] = img8
 
+    def render_frames(self, cams, cfg, images, images256, first_pass, pass_count, write_u8=0):
+        assert first_pass == 1
+        px = pt.owned_pixels(self.w, self.h, *self.tiling)
+        for f, cam in enumerate(cams):
+            img, img8, _ = oracle.render(self.scene.view, cam, cfg, first_pass, pass_count, pixels=px)
+            images[f].numpy().reshape(-1, 3)[px] = img
+            if write_u8 and images256 is not None:
+                images256[f].numpy().reshape(-1, 3)[px] = img8
+
     def synchronize(self):
         pass
 
     def finalize_u8(self, cfg, pass_):
         self.img8[:] = oracle.gamma_u8(cfg, self.img, pass_)
+
+    def finalize_u8_image(self, cfg, pass_, image, image256):
+        image256.numpy().reshape(-1, 3)[:] = oracle.gamma_u8(cfg, image.numpy().reshape(-1, 3), pass_)
 
 
 def _scene():
@@ -95,6 +107,50 @@ def _worker(rank, world, port, out_dir, collective="gather", inflight=1):
                  owned=pt.owned_pixels(W, H, BAND, world, rank))
     finally:
         dist.destroy_process_group()
+
+
+CAM_YAWS = (0.0, 0.5, -0.6)
+
+
+def _group_worker(rank, world, port, out_dir, collective):
+    """bench.py's frame groups (PT_BENCH_GROUP): FrameGroup renders up to three frames per launch, each through
+    its own camera, and moves them with one collective; a launch of fewer frames follows a full one."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        scene = _scene()
+        cfg, _ = _setup()
+        cams = [pt.camera(W, H, yaw=y, pitch=0.08, radius=12.5, center=(0, 1.2, 0)) for y in CAM_YAWS]
+        g = pt.FrameGroup(OracleFrameRenderer(scene), W, H, 3, dist, BAND, device="cpu", collective=collective)
+        g.launch(cams, cfg, SPP)
+        g.synchronize()
+        full = [g.download(f) for f in range(3)]
+        g.launch(cams[1:], cfg, SPP)  # two frames: the stack's third frame is left as it was
+        g.synchronize()
+        two = [g.download(f) for f in range(2)]
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), img=np.stack([a for a, _ in full]),
+                 img8=np.stack([b for _, b in full]), img2=np.stack([a for a, _ in two]),
+                 img82=np.stack([b for _, b in two]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,collective", [(2, "gather"), (3, "gather"), (2, "reduce")])
+def test_frame_group_equals_single_renders(tmp_path, world, collective):
+    mp.start_processes(_group_worker, args=(world, _free_port(), str(tmp_path), collective), nprocs=world,
+                       join=True, start_method="spawn")
+    r0 = np.load(tmp_path / "rank0.npz")
+    cfg, _ = _setup()
+    scene = _scene()  # keep alive: the view points into it
+    for f, y in enumerate(CAM_YAWS):
+        cam = pt.camera(W, H, yaw=y, pitch=0.08, radius=12.5, center=(0, 1.2, 0))
+        ref, ref8, _ = oracle.render(scene.view, cam, cfg, 1, SPP)
+        assert np.array_equal(r0["img"][f].reshape(-1, 3).view(np.uint32), ref.view(np.uint32)), f
+        assert np.array_equal(r0["img8"][f].reshape(-1, 3), ref8), f
+        if f >= 1:
+            assert np.array_equal(r0["img2"][f - 1].reshape(-1, 3).view(np.uint32), ref.view(np.uint32)), f
+            assert np.array_equal(r0["img82"][f - 1].reshape(-1, 3), ref8), f
 
 
 def _free_port():

@@ -33,6 +33,9 @@ def main() -> None:
                     help="passes per rendered frame (default the workload's 8); ms figures are per 8 passes (one "
                          "metric frame), so a 32-pass frame with PT_PASS_BATCH=32 tells what one launch for four "
                          "frames would cost")
+    ap.add_argument("--group", type=int, default=1,
+                    help="frames per launch (pt_render_frames): each render call renders this many frames of the "
+                         "view; ms figures stay per frame")
     args = ap.parse_args()
     wl = bench.Workload("metric")
     spp = args.spp or wl.spp
@@ -45,6 +48,20 @@ def main() -> None:
         r.setup_frame(wl.width, wl.height)
         rs.append(r)
     r = rs[0]
+    bufs = {}
+    if args.group > 1:
+        import torch
+
+        for q in rs:
+            bufs[id(q)] = [torch.zeros(wl.width * wl.height * 3, dtype=torch.float32, device="cuda:0")
+                           for _ in range(args.group)]
+
+    def draw(q) -> None:
+        if args.group > 1:
+            q.render_frames([wl.cam] * args.group, wl.cfg, bufs[id(q)], None, 1, spp, write_u8=0)
+        else:
+            q.render(wl.cam, wl.cfg, 1, spp, write_u8=0)
+
     out = {}
     base = None
     for n in [int(x) for x in args.counts.split(",")]:
@@ -54,15 +71,15 @@ def main() -> None:
                 q.set_tiling(args.band_rows or bench.BAND_ROWS, n, k)
                 if args.order:
                     q.order_bands_by_cost(wl.cam, wl.cfg, wl.spp, regions=args.deal)
-                q.render(wl.cam, wl.cfg, 1, spp, write_u8=0)  # warm
+                draw(q)  # warm
                 q.synchronize()
                 q.stats_reset()
             t0 = time.perf_counter()
             for f in range(args.frames):
-                rs[f % len(rs)].render(wl.cam, wl.cfg, 1, spp, write_u8=0)
+                draw(rs[f % len(rs)])
             for q in rs:
                 q.synchronize()
-            per_rank.append((time.perf_counter() - t0) / args.frames * 1e3 * scale)
+            per_rank.append((time.perf_counter() - t0) / (args.frames * args.group) * 1e3 * scale)
             kms, kn = r.kernel_time_kind(0)
             kern.append(kms / max(kn, 1))
         if base is None:
