@@ -417,14 +417,16 @@ def main() -> int:
     ms_per_step = elapsed / args.steps * 1000.0
     avg_launch_s = solo_ms / max(solo_launches, 1) / 1000.0  # one frame at a time (see above)
     launches_per_frame = launches / max(args.steps, 1)
+    # the roofline prices the solo launch, which renders ONE frame; with frame groups a timed launch renders G
+    frame_launches = launches_per_frame * group
     if schedule == "persistent":
         # one launch = a batch of passes over the frame (this rank's bands when tiled)
         bytes_per_launch = algorithmic_bytes(counts, scene.view.sphere_num, cfg.bvh_leaf_node_triangle_num,
-                                             width * height, spp) / world / launches_per_frame
+                                             width * height, spp) / world / frame_launches
         kernel_name = r.last_kernel()
     else:
         # one launch = one depth of one pass
-        bytes_per_launch = extend_bytes(counts, scene.view.sphere_num) / world / launches_per_frame
+        bytes_per_launch = extend_bytes(counts, scene.view.sphere_num) / world / frame_launches
         kernel_name = "extend_kernel<LEAF1=true,STATS=false>"
     workload = wl.key
     key = workload + ("" if schedule == "persistent" else "/wavefront")
@@ -446,7 +448,7 @@ def main() -> int:
     valu_achieved = valu_insts / avg_launch_s / 1e9 if valu_insts else None
     # The same instructions over the timed mode's own clock: VALU per frame / ms_per_step (frames in flight
     # overlap, so this is what the timed figure implies per GPU; it can never exceed 1)
-    valu_timed = valu_insts * launches_per_frame / (ms_per_step / 1000.0) / 1e9 if valu_insts else None
+    valu_timed = valu_insts * frame_launches / (ms_per_step / 1000.0) / 1e9 if valu_insts else None
     # Lane-weighted: a wave-instruction counts active lanes / 64 (PT_UPROF lanes per phase x the PT_DUP VALU
     # split per phase, tools/lane_weighted.py, recorded in profiles/traffic.json)
     valu_lanes = float(prof["valu_lane_weighted_per_launch"]) * scale if prof.get("valu_lane_weighted_per_launch") else None

@@ -1,4 +1,5 @@
-# Rehearsal of the N > 1 bench path on a one-GPU box: 2, 4 and 8 ranks gathering and 3 reducing over gloo,
+# Rehearsal of the N > 1 bench path on a one-GPU box: 2, 4 and 8 ranks gathering and 3 reducing over gloo
+# (and 2 reducing, 4 and 8 gathering with frame groups),
 # every rank on device 0. Each bench line carries config.image_matches_1gpu (rank 0 re-renders the frame
 # alone and compares bitwise) and bench.py exits 3 on a mismatch; the saved 8-bit images must also equal the
 # 1-GPU image.
@@ -9,14 +10,19 @@ export TMPDIR=/tmp
 TAG=${1:-mr}
 mkdir -p gpurun_out/$TAG
 timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --save-image gpurun_out/$TAG/n1.png > gpurun_out/$TAG/b1.json 2>/dev/null || exit $?
-run() {  # ranks port extra-env...
-  n=$1; port=$2; shift 2
-  env "$@" PT_BENCH_BACKEND=gloo PT_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $port bench.py --gpus $n --steps 3 --warmup 1 --save-image gpurun_out/$TAG/n$n.png > gpurun_out/$TAG/b$n.json 2> gpurun_out/$TAG/b$n.err || exit $?
-  python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], 'ranks: image_matches_1gpu', d['config']['image_matches_1gpu'], d['value'], 'Mrays/s')" gpurun_out/$TAG/b$n.json $n
-  cmp gpurun_out/$TAG/n1.png gpurun_out/$TAG/n$n.png || exit 4
+run() {  # name ranks port extra-env...
+  m=$1; n=$2; port=$3; shift 3
+  env "$@" PT_BENCH_BACKEND=gloo PT_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $port bench.py --gpus $n --steps 5 --warmup 1 --save-image gpurun_out/$TAG/$m.png > gpurun_out/$TAG/$m.json 2> gpurun_out/$TAG/$m.err || exit $?
+  python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], 'ranks: image_matches_1gpu', d['config']['image_matches_1gpu'], 'frames per launch', d['config']['frames_per_launch'], d['value'], 'Mrays/s')" gpurun_out/$TAG/$m.json $n
+  cmp gpurun_out/$TAG/n1.png gpurun_out/$TAG/$m.png || exit 4
 }
-run 2 29533 PT_FRAME_COLLECTIVE=gather
-run 3 29534 PT_FRAME_COLLECTIVE=reduce
-run 4 29535 PT_FRAME_COLLECTIVE=gather
-run 8 29536 PT_FRAME_COLLECTIVE=gather
+# frame groups (PT_BENCH_GROUP: G frames per launch, one collective per group): 5 steps = a launch of G
+# frames and one of the rest
+run b2 2 29533 PT_FRAME_COLLECTIVE=gather
+run b3 3 29534 PT_FRAME_COLLECTIVE=reduce
+run b4 4 29535 PT_FRAME_COLLECTIVE=gather
+run b8 8 29536 PT_FRAME_COLLECTIVE=gather
+run g2 2 29537 PT_FRAME_COLLECTIVE=reduce PT_BENCH_GROUP=4
+run g4 4 29538 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=4
+run g8 8 29539 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=4
 echo "saved images identical to the 1-GPU image"

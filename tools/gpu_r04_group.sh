@@ -38,4 +38,8 @@ for r in 1 2; do
   ARGS="--counts 2 --ranks-max 1 --frames 8 --inflight 3 --share 50 --group 2" run s2_g2_f3_$r PT_TRI_MIN=3
   ARGS="--counts 2 --ranks-max 1 --frames 6 --inflight 3 --share 50 --group 4" run s2_g4_f3_$r PT_TRI_MIN=3
 done
+for g in 1 4; do
+  timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d gpurun_out/$TAG/pmc_s8_g$g -o run -- python3 tools/share_render.py --n 8 --group $g > gpurun_out/$TAG/pmc_s8_g$g.log 2>&1 || exit $?
+  grep "share 0" gpurun_out/$TAG/pmc_s8_g$g.log | tee -a gpurun_out/$TAG/summary.txt
+done
 echo done

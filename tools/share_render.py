@@ -21,17 +21,28 @@ def main() -> None:
     ap.add_argument("--n", type=int, required=True)
     ap.add_argument("--frames", type=int, default=4)
     ap.add_argument("--workload", default="metric")
+    ap.add_argument("--group", type=int, default=1, help="frames per launch (pt_render_frames)")
     args = ap.parse_args()
     wl = bench.Workload(args.workload)
     r = pt.Renderer(0)
     r.upload(wl.scene, wl.cfg)
     r.setup_frame(wl.width, wl.height)
     r.set_tiling(bench.BAND_ROWS, args.n, 0)
+    bufs = None
+    if args.group > 1:
+        import torch
+
+        bufs = [torch.zeros(wl.width * wl.height * 3, dtype=torch.float32, device="cuda:0")
+                for _ in range(args.group)]
     for _ in range(args.frames):
-        r.render(wl.cam, wl.cfg, 1, wl.spp, write_u8=0)
+        if bufs:
+            r.render_frames([wl.cam] * args.group, wl.cfg, bufs, None, 1, wl.spp, write_u8=0)
+        else:
+            r.render(wl.cam, wl.cfg, 1, wl.spp, write_u8=0)
         r.synchronize()
     ms, n = r.kernel_time_kind(0)
-    print(f"share 0 of {args.n}: {ms / max(n, 1):.3f} ms per launch over {n} launches ({r.last_kernel()})")
+    print(f"share 0 of {args.n}: {ms / max(n, 1):.3f} ms per launch of {args.group} frame(s) over {n} launches "
+          f"({r.last_kernel()})")
     r.close()
 
 
