@@ -23,6 +23,7 @@ struct PassChoice {
     bool leaf1, stats;
     int feat;
     bool il;  // the inline-leaf copy of the node array exists (every leaf's skip index is the next record)
+    bool multi = false;  // a pt_render_frames launch (several frames): pass_kernel_u's MULTI instance
 };
 // whether launch_pass runs pass_kernel_u for this choice (its node array may then be the inline-leaf copy)
 bool pass_uses_unified(const PassChoice& pc, int lds_bytes);

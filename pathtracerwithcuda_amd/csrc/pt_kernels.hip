@@ -320,7 +320,9 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
 // batches, lanes in triangle batches, lanes refilled, then cycles and the drained/ready/idle counts,
 // and the launch timeline in stats[32..41].
 // FEAT: the scene features shade_hit can reach (pt_path.h PT_FEAT_*).
-template <int MINW, bool PROF, int FEAT>
+// MULTI: the pt_render_frames instance (several frames per launch, LANE_GEN refills); the single-frame
+// instances keep the refill without that state (2 % faster on the bench frame, profiles/r04/group/)
+template <int MINW, bool PROF, int FEAT, bool MULTI = false>
 __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
                                                                 int walk_steps, int tri_min, int walk_min) {
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     Counters none = {0u, 0u, 0u, 0u, 0u, 0u};
     // the units of one frame copy; a pt_render_frames launch has `frames` copies one after another
     const unsigned int frame_units = (unsigned int)P0->til.unit_count << batch_log2;
-    const unsigned int units = frame_units * (unsigned int)max(1, P0->out.frames);
+    const unsigned int units = MULTI ? frame_units * (unsigned int)max(1, P0->out.frames) : frame_units;
     const EvenRegions regions{units, (units + PT_SHARDS - 1) / PT_SHARDS};
     WorkCursor cursor = work_begin();
     bool drained = false;
@@ -423,17 +425,37 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (want) {
                 if (u != ~0u) {
                     unit = u;
-                    mode = LANE_GEN;
+                    if (MULTI) {
+                        mode = LANE_GEN;
+                    } else {
+                        const int pixel = unit_to_pixel(til, u >> batch_log2);
+                        const int32_t hseed = hash_pt(first_pass + (int)(u & ((1u << batch_log2) - 1u)));
+                        const DevCamera cam = load_const(&P->cam);
+                        if (PT_DUP == 4) {
+                            PathState p2; int px2 = pixel, hs2 = hseed;
+                            opaque(px2); opaque(hs2);
+                            generate_path(cam, cfg, px2, hs2, &p2);
+                            opaque(p2);
+                        }
+                        generate_path(cam, cfg, pixel, hseed, &ps);
+                        pseed = path_seed(hseed, pixel);
+                        depth = 0;
+                        if (cfg.max_depth > 0) {
+                            mode = LANE_NEW;
+                        } else {
+                            finish_unit(til, cfg, out, ps, unit, u, first_pass, write_u8, batch_log2, clamp_hi, depth);
+                        }
+                    }
                 } else if (drained) {
                     mode = LANE_DONE;
                 }
             }
         }
-        // lanes holding a new unit start its camera path. The camera is read through the scalar cache, so one
-        // refill starts the paths of one frame (pt_render_frames): those of the first such lane's frame; a lane
-        // whose unit lies in another frame (a refill that spans two frames' units) starts in the next round
-        const unsigned long long gen_mask = __ballot(mode == LANE_GEN);
-        if (gen_mask) {
+        // MULTI: lanes holding a new unit start its camera path. The camera is read through the scalar cache, so
+        // one refill starts the paths of one frame: those of the first such lane's frame; a lane whose unit lies
+        // in another frame (a refill that spans two frames' units) starts in the next round
+        const unsigned long long gen_mask = MULTI ? __ballot(mode == LANE_GEN) : 0ull;
+        if (MULTI && gen_mask) {
             unsigned int lu = unit;  // the unit within its frame
             int frame = 0;
             if (mode == LANE_GEN) {
@@ -443,13 +465,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (mode == LANE_GEN && frame == f0) {
                 const int pixel = unit_to_pixel(til, lu >> batch_log2);
                 const int32_t hseed = hash_pt(first_pass + (int)(lu & ((1u << batch_log2) - 1u)));
-                const DevCamera cam = load_const((out.frames > 1 ? out.cams : &P->cam) + f0);
-                if (PT_DUP == 4) {
-                    PathState p2; int px2 = pixel, hs2 = hseed;
-                    opaque(px2); opaque(hs2);
-                    generate_path(cam, cfg, px2, hs2, &p2);
-                    opaque(p2);
-                }
+                const DevCamera cam = load_const(out.cams + f0);
                 generate_path(cam, cfg, pixel, hseed, &ps);
                 pseed = path_seed(hseed, pixel);
                 depth = 0;
@@ -493,7 +509,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (mode == LANE_READY) {  // the pass's end for this unit, or the next trace step
                 depth++;
                 if (!alive || depth >= cfg.max_depth) {
-                    finish_unit(til, cfg, out, ps, unit, frame_local(unit, frame_units), first_pass, write_u8, batch_log2, clamp_hi, depth);
+                    finish_unit(til, cfg, out, ps, unit, MULTI ? frame_local(unit, frame_units) : unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
                     mode = LANE_WANT;
                 } else {
                     mode = LANE_NEW;  // its next segment starts in the next round's refill, with the new paths
@@ -884,10 +900,22 @@ using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int,
 // pass_kernel_u specialised on the scene's features (pt_path.h PT_FEAT_*): feat is what the scene can reach;
 // PT_FEAT_SPECIALISE=0 keeps the all-features kernel. `feat_used` receives the instance's features, so the
 // kernel description names the kernel that runs. PT_UPROF=1: the profiling instance (6 waves, all features).
-static PassFnU pass_fn_u(int minw, int feat, int* feat_used, int* minw_used) {
+// multi: the MULTI instance of the feature set's default wave count (pt_render_frames; PT_MIN_WAVES and
+// PT_UPROF do not apply to it).
+static PassFnU pass_fn_u(int minw, int feat, bool multi, int* feat_used, int* minw_used) {
     static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
     static const int prof = env_int("PT_UPROF", 0, 0, 1);
     if (!spec) feat = PT_FEAT_ALL;
+    if (multi) {
+        *feat_used = feat;
+        *minw_used = (feat & PT_FEAT_MEDIUM) ? 6 : 7;
+        switch (feat) {
+            case 0: return pass_kernel_u<7, false, 0, true>;
+            case 1: return pass_kernel_u<6, false, 1, true>;
+            case 2: return pass_kernel_u<7, false, 2, true>;
+            default: return pass_kernel_u<6, false, 3, true>;
+        }
+    }
     if (prof) { *feat_used = PT_FEAT_ALL; *minw_used = 6; return pass_kernel_u<6, true, PT_FEAT_ALL>; }
     *feat_used = feat;
     *minw_used = minw;
@@ -973,7 +1001,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
         static const int tri_min = env_int("PT_TRI_MIN", 4, 1, 64);
         static const int walk_min = env_int("PT_WALK_MIN", 8, 0, 64);
         int fu, wu;
-        const PassFnU fn = pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, &fu, &wu);
+        const PassFnU fn = pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, pc.multi, &fu, &wu);
         const LaunchParams* a0 = params_dev;
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
             a8 = walk_min;
@@ -1014,9 +1042,10 @@ std::string pass_kernel_desc(const PassChoice& pc, int lds_bytes) {
     char buf[160];
     if (use_unified(pc, lds_bytes)) {
         int fu, wu;
-        (void)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, &fu, &wu);
+        (void)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, pc.multi, &fu, &wu);
         static const int prof = env_int("PT_UPROF", 0, 0, 1);
-        std::snprintf(buf, sizeof(buf), "pass_kernel_u<MINW=%d,FEAT=%d%s>", wu, fu, prof ? ",PROF" : "");
+        std::snprintf(buf, sizeof(buf), "pass_kernel_u<MINW=%d,FEAT=%d%s>", wu, fu,
+                      pc.multi ? ",MULTI" : prof ? ",PROF" : "");
     } else {
         std::snprintf(buf, sizeof(buf), "pass_kernel<LEAF1=%d,STATS=%d,MINW=%d>", pc.leaf1 ? 1 : 0, pc.stats ? 1 : 0,
                       pass_min_waves(false, pc.feat));
@@ -1031,7 +1060,7 @@ int pass_grid_size(const PassChoice& pc, int lds_bytes) {
     if (cus <= 0) cus = 256;
     const bool u = use_unified(pc, lds_bytes);
     int fu, wu;
-    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, &fu, &wu)
+    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, pc.multi, &fu, &wu)
                        : (const void*)pass_fn(pc.leaf1, pc.stats, pass_min_waves(false, pc.feat));
     const size_t lds = u ? (size_t)lds_bytes : 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, u ? PT_UBLOCK : PT_BLOCK, lds) != hipSuccess || blocks <= 0)

@@ -1104,8 +1104,9 @@ int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, con
     for (int f = 1; f < frames; f++)
         if ((int)cams[f].resolution.x != ctx->width) { set_error("camera width != frame width"); return PT_E_ARG; }
     const int feat = render_feat(ctx, lp.cfg);
-    const PassChoice pc = pass_choice(ctx, feat);
+    PassChoice pc = pass_choice(ctx, feat);
     const bool fused = frames > 1 && !wavefront_schedule(ctx) && pass_uses_unified(pc, pass_lds_bytes(ctx));
+    pc.multi = fused;
     if (!fused) {
         float* const img0 = ctx->image;
         uint8_t* const img8 = ctx->image256;

@@ -16,13 +16,14 @@ run() {  # name ranks port extra-env...
   python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], 'ranks: image_matches_1gpu', d['config']['image_matches_1gpu'], 'frames per launch', d['config']['frames_per_launch'], d['value'], 'Mrays/s')" gpurun_out/$TAG/$m.json $n
   cmp gpurun_out/$TAG/n1.png gpurun_out/$TAG/$m.png || exit 4
 }
-# frame groups (PT_BENCH_GROUP: G frames per launch, one collective per group): 5 steps = a launch of G
-# frames and one of the rest
-run b2 2 29533 PT_FRAME_COLLECTIVE=gather
-run b3 3 29534 PT_FRAME_COLLECTIVE=reduce
-run b4 4 29535 PT_FRAME_COLLECTIVE=gather
-run b8 8 29536 PT_FRAME_COLLECTIVE=gather
-run g2 2 29537 PT_FRAME_COLLECTIVE=reduce PT_BENCH_GROUP=4
-run g4 4 29538 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=4
-run g8 8 29539 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=4
+# b*: one frame per launch (PT_BENCH_GROUP=1); g*: the default frame groups at N > 1 (4 frames per launch at
+# 2-3 ranks, 8 at 4+, one collective per group): 5 steps = one launch of 4 frames and one of 1, or one of 5
+run b2 2 29533 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=1
+run b3 3 29534 PT_FRAME_COLLECTIVE=reduce PT_BENCH_GROUP=1
+run b4 4 29535 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=1
+run b8 8 29536 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=1
+run g2 2 29537 PT_FRAME_COLLECTIVE=reduce
+run g3 3 29538 PT_FRAME_COLLECTIVE=gather
+run g4 4 29539 PT_FRAME_COLLECTIVE=gather
+run g8 8 29540 PT_FRAME_COLLECTIVE=gather
 echo "saved images identical to the 1-GPU image"

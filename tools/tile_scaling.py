@@ -36,6 +36,9 @@ def main() -> None:
     ap.add_argument("--group", type=int, default=1,
                     help="frames per launch (pt_render_frames): each render call renders this many frames of the "
                          "view; ms figures stay per frame")
+    ap.add_argument("--total", type=int, default=0,
+                    help="with --group: render this many frames in launches of at most --group frames (bench.py's "
+                         "timed sequence, e.g. 20 = 8 + 8 + 4) instead of --frames full launches")
     args = ap.parse_args()
     wl = bench.Workload("metric")
     spp = args.spp or wl.spp
@@ -56,11 +59,16 @@ def main() -> None:
             bufs[id(q)] = [torch.zeros(wl.width * wl.height * 3, dtype=torch.float32, device="cuda:0")
                            for _ in range(args.group)]
 
-    def draw(q) -> None:
+    def draw(q, n=None) -> None:
+        n = n or args.group
         if args.group > 1:
-            q.render_frames([wl.cam] * args.group, wl.cfg, bufs[id(q)], None, 1, spp, write_u8=0)
+            q.render_frames([wl.cam] * n, wl.cfg, bufs[id(q)][:n], None, 1, spp, write_u8=0)
         else:
             q.render(wl.cam, wl.cfg, 1, spp, write_u8=0)
+
+    launches = ([min(args.group, args.total - i) for i in range(0, args.total, args.group)] if args.total
+                else [args.group] * args.frames)
+    nframes = sum(launches)
 
     out = {}
     base = None
@@ -75,11 +83,11 @@ def main() -> None:
                 q.synchronize()
                 q.stats_reset()
             t0 = time.perf_counter()
-            for f in range(args.frames):
-                draw(rs[f % len(rs)])
+            for f, g in enumerate(launches):
+                draw(rs[f % len(rs)], g)
             for q in rs:
                 q.synchronize()
-            per_rank.append((time.perf_counter() - t0) / (args.frames * args.group) * 1e3 * scale)
+            per_rank.append((time.perf_counter() - t0) / nframes * 1e3 * scale)
             kms, kn = r.kernel_time_kind(0)
             kern.append(kms / max(kn, 1))
         if base is None:
