@@ -346,10 +346,11 @@ struct Counters {
 // exact 32-B node records (the reference's own node sequence: the STATS kernels count its visits).
 template <bool LEAF1, bool STATS>
 __device__ __forceinline__ bool mesh_closest(const DevScene& sc, int begin, int end, v3 o, v3 d, v3 inv,
-                                             float* ht, float* ht1, float* ht2, int* htri, Counters* ctr) {
+                                             float* ht, float* ht1, float* ht2, int* htri, Counters* ctr,
+                                             float t0 = __builtin_inff()) {
     const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
     const __amdgpu_buffer_rsrc_t rt = make_rsrc(sc.tri_geom, sc.tri_count * 48);
-    float min_t = __builtin_inff();
+    float min_t = t0;  // infinity, or the medium bound (medium_bound)
     float min_t1 = 0.0f, min_t2 = 0.0f;
     int min_tri = -1;
     bool hit = false;
@@ -573,8 +574,9 @@ struct Hit {
     int prim;
 };
 
+// t0: every mesh walk's starting min_t (infinity; the medium bound in the medium-bounded mode)
 template <bool LEAF1, bool STATS>
-__device__ __forceinline__ Hit closest_hit(const DevScene& sc, v3 o, v3 d, Counters* ctr) {
+__device__ __forceinline__ Hit closest_hit(const DevScene& sc, v3 o, v3 d, Counters* ctr, float t0 = __builtin_inff()) {
     Hit h;
     h.t = __builtin_inff(); h.t1 = __builtin_inff(); h.t2 = __builtin_inff();
     h.type = 0; h.prim = -1;
@@ -590,7 +592,7 @@ __device__ __forceinline__ Hit closest_hit(const DevScene& sc, v3 o, v3 d, Count
             const int2 r = uniform_ptr(sc.mesh_range)[m];
             float t, t1, t2;
             int tri;
-            const bool mh = mesh_closest<LEAF1, STATS>(sc, r.x, r.y, o, d, inv, &t, &t1, &t2, &tri, ctr);
+            const bool mh = mesh_closest<LEAF1, STATS>(sc, r.x, r.y, o, d, inv, &t, &t1, &t2, &tri, ctr, t0);
             if (mh && t < h.t && t > 0.0f) {
                 h.t = t; h.t1 = t1; h.t2 = t2; h.prim = tri; h.type = 2;
             }
@@ -646,10 +648,13 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
 // One invocation of trace_ray_kernel for one live ray (path_tracer_kernel.cu:381-625).
 // pseed = path_seed(hash(pass), pixel). Returns false when the reference would write -1 into
 // energy_exist_pixels.
+// In the medium-bounded mode the walks start at the segment's medium bound, as in pass_kernel_u (so the
+// instrumented kernel counts the bounded walk's nodes and triangle tests).
 template <bool LEAF1, bool STATS>
 __device__ __forceinline__ bool trace_step(const DevScene& sc, const DevConfig& cfg, int depth, int32_t pseed,
                                            PathState* ps, Counters* ctr) {
-    const Hit h = closest_hit<LEAF1, STATS>(sc, ps->o, ps->d, ctr);
+    const float t0 = cfg.medium_bound ? medium_bound(sc, cfg, ps->medium, depth, pseed) : __builtin_inff();
+    const Hit h = closest_hit<LEAF1, STATS>(sc, ps->o, ps->d, ctr, t0);
     return shade_hit<STATS>(sc, cfg, depth, pseed, ps, h, ctr);
 }
 

@@ -453,9 +453,23 @@ def test_medium_bound_mode_variants(bench_gpu):
             img, img8 = r.download()
         finally:
             r.set_medium_bound(None)
-        ref, ref8, _ = oracle.render(sc.view, cam, cfg, 1, 2, medium_bound=True)
+        ref, ref8, st = oracle.render(sc.view, cam, cfg, 1, 2, medium_bound=True)
         assert_bitwise(img.reshape(-1, 3), ref, "bounded variant float")
         assert_bitwise(img8.reshape(-1, 3), ref8, "bounded variant 8-bit")
+        # the instrumented kernel walks the bounded walk too: its node and triangle counts (the bench line's
+        # counts_per_frame under --medium-bound) are the oracle's bounded counts
+        r.set_medium_bound(True)
+        r.set_instrumented(True)
+        try:
+            r.stats_reset()
+            r.render(cam, cfg, 1, 2, write_u8=2)
+            img_i, _ = r.download()
+            got = r.stats()
+        finally:
+            r.set_instrumented(False)
+            r.set_medium_bound(None)
+        assert_bitwise(img_i.reshape(-1, 3), ref, "bounded instrumented float")
+        assert got == {"segments": st["segments"], "nodes": st["nodes"], "tris": st["tris"]}
 
 
 def test_c5_4k_textured_depth12_frame(bench_gpu):

@@ -22,9 +22,12 @@ def main() -> None:
     ap.add_argument("--frames", type=int, default=4)
     ap.add_argument("--workload", default="metric")
     ap.add_argument("--group", type=int, default=1, help="frames per launch (pt_render_frames)")
+    ap.add_argument("--medium-bound", action="store_true", help="pt_set_medium_bound (tolerance mode)")
     args = ap.parse_args()
     wl = bench.Workload(args.workload)
     r = pt.Renderer(0)
+    if args.medium_bound:
+        r.set_medium_bound(True)
     r.upload(wl.scene, wl.cfg)
     r.setup_frame(wl.width, wl.height)
     r.set_tiling(bench.BAND_ROWS, args.n, 0)
