@@ -281,16 +281,19 @@ def main() -> int:
     # (+0.27 %, 3 of 3 rounds, profiles/r03/grid_share/). Not for the 0.4-4 s C4/C5 frames, whose tails are
     # a small part of them: there the 10 % left to the third frame sits idle (C4 -3.8 %)
     # Frames per launch (pt_render_frames, pathtracerwithcuda_amd.FrameGroup): each context renders G frames of
-    # the view in one pass launch and moves them with one collective, so a small share pays one launch's start
-    # and tail per G frames. Every frame is still rendered whole, with its own 8-bit output.
-    # Measured per frame of rank 0's share over the timed sequence of 20 frames (tools/tile_scaling.py --total,
-    # profiles/r04/group/), two contexts on the whole grid: 8-way 0.744-0.750 ms with 8 frames per launch
-    # (8 + 8 + 4) against 0.877-0.895 one frame per launch on five contexts on quarter grids (0.793-0.800 with
-    # 4 per launch on three half grids); 4-way 1.371-1.372 vs 1.551-1.555 (8 per launch); 2-way 2.690-2.693 vs
-    # 2.863-2.867 (4 per launch). The whole frame is slower grouped (5.46 ms with 2, 5.91 with 4, vs 5.41): one
-    # frame per launch at N = 1, and for the 0.4-4 s C4/C5 frames, whose tails are a small part of them.
-    group = int(os.environ.get("PT_BENCH_GROUP", "0")) or (1 if world == 1 or heavy else 4 if world <= 3 else 8)
-    inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or (3 if world == 1 else 5 if group == 1 else 2)
+    # the view in one pass launch (and, tiled, moves them with one collective), so the frames share one launch's
+    # start and tail. Every frame is still rendered whole, with its own 8-bit output. Measured
+    # (profiles/r04/group/), two contexts on the whole grid against one frame per launch on three (N = 1, 45 %
+    # grids) or five (tiled, 25 %) contexts: the bench line at N = 1 13662-13697 Mrays/s with 8 frames per
+    # launch (8 + 8 + 4 over 20 steps) vs 13441-13475 (4: 13534-13550, 10: 13603-13638); rank 0's share per
+    # frame over 20 frames (tools/tile_scaling.py --total 20) 8-way 0.744-0.750 ms vs 0.877-0.895, 4-way
+    # 1.371-1.372 vs 1.551-1.555 (8 per launch), 2-way 2.690-2.693 vs 2.863-2.867 (4 per launch). Not for the
+    # 0.1-ms C1 frame (27132-27561 vs 33068-33337 with 4 per launch: host-bound) nor the 0.4-4 s C4/C5 frames,
+    # whose tails are a small part of them.
+    group = int(os.environ.get("PT_BENCH_GROUP", "0")) or (
+        1 if heavy or args.workload == "c1" else 4 if world in (2, 3) else 8)
+    inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or (
+        2 if group > 1 else 3 if world == 1 else 5)
     grid_share = int(os.environ.get("PT_BENCH_GRID_SHARE", "0")) or (
         (45 if inflight == 3 and not heavy and group == 1 else 100 // (inflight - 1)) if inflight >= 3 else 100)
     wl = Workload(args.workload)

@@ -656,15 +656,16 @@ def test_edge_cases(gpu, case):
 def test_render_frames_equal_separate_frames(gpu, case):
     """pt_render_frames: several frames, each through its own camera, in one pass launch per batch of passes
     (the persistent schedule; the wavefront schedule renders them one after another). Every frame is the
-    oracle's frame of its camera bit for bit, 8-bit output included: a refill whose units span two frames
-    generates one frame's paths and the other frame's in the next round, and frame f's radiances are summed
-    into its own image. Cases: one 8-pass launch; a continuation range 2..4 (batches of 2 and 1, the
-    one-pass launch through pass_rad too); a 3-band share (rows of band 1 only); a 45 % grid."""
+    oracle's frame of its camera bit for bit, 8-bit output included, and frame f's radiances are summed into
+    its own image. Cases: one 8-pass launch; a continuation range 2..4 (batches of 2 and 1, the
+    one-pass launch through pass_rad too); a 3-band share (rows of band 1 only); a 45 % grid. The frames' units
+    are laid out in 64-unit blocks (pt_scene.h multi_frame_stride) and a refill takes one block's units, so all
+    of its new paths share a frame and a camera."""
     import torch
 
     sc = pt.cornell_scene(pt.torus_knot(60, 16), cube_length=32)
     cfg = pt.configuration(max_tracer_depth=6)
-    W, H = 72, 48
+    W, H = 70, 45  # 3150 pixels: a frame's units are not a whole number of 64-unit blocks (padding skipped)
     cams = [pt.camera(W, H, yaw=y, **BENCH_CAM) for y in (0.0, 0.4, -0.7)]
     first, count = (2, 3) if case == "odd_range" else (1, 8)
     gpu.upload(sc, cfg)
