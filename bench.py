@@ -426,8 +426,10 @@ def main() -> int:
     ms_per_step = elapsed / args.steps * 1000.0
     avg_launch_s = solo_ms / max(solo_launches, 1) / 1000.0  # one frame at a time (see above)
     launches_per_frame = launches / max(args.steps, 1)
-    # the roofline prices the solo launch, which renders ONE frame; with frame groups a timed launch renders G
-    frame_launches = launches_per_frame * group
+    # the roofline prices the solo launch, which renders ONE frame; with frame groups a timed launch renders up
+    # to G frames: pass launches per frame = pass launches per group launch (every frame of a group takes the
+    # same batches of passes)
+    frame_launches = launches / max(1, -(-args.steps // group))
     if schedule == "persistent":
         # one launch = a batch of passes over the frame (this rank's bands when tiled)
         bytes_per_launch = algorithmic_bytes(counts, scene.view.sphere_num, cfg.bvh_leaf_node_triangle_num,

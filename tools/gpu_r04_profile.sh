@@ -21,13 +21,13 @@ done
 timeout -k 10 500 python3 bench.py --workload c4 --medium-bound --no-cpu-baseline > gpurun_out/$TAG/wl_c4_mb.json 2> gpurun_out/$TAG/wl_c4_mb.err || exit $?
 cut -c1-160 gpurun_out/$TAG/wl_c4_mb.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$TAG/trace_inflight -o run -- $B > gpurun_out/$TAG/trace_inflight.log 2>&1 || exit $?
-export PT_BENCH_INFLIGHT=1
+export PT_BENCH_INFLIGHT=1 PT_BENCH_GROUP=1  # one frame per launch, one at a time: the roofline's solo launch
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$TAG/trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/$TAG/trace.log 2>&1 || exit $?
 P="python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/$TAG/pmc_fetch -o run -- $P > gpurun_out/$TAG/pmc_fetch.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/$TAG/pmc_write -o run -- $P > gpurun_out/$TAG/pmc_write.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/$TAG/pmc_sq -o run -- $P > gpurun_out/$TAG/pmc_sq.log 2>&1 || exit $?
-unset PT_BENCH_INFLIGHT
+unset PT_BENCH_INFLIGHT PT_BENCH_GROUP
 timeout -k 10 120 python3 tools/uprof.py metric > gpurun_out/$TAG/uprof_metric.json 2> gpurun_out/$TAG/uprof_metric.err || exit $?
 if [ -d pathtracerwithcuda_amd/lib_dup1 ]; then
   bash tools/gpu_dup.sh $TAG/dup > gpurun_out/$TAG/dup.log 2>&1 || exit $?
