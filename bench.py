@@ -290,13 +290,15 @@ def main() -> int:
     # 1.371-1.372 vs 1.551-1.555 (8 per launch), 2-way 2.690-2.693 vs 2.863-2.867 (4 per launch). Not for the
     # 0.1-ms C1 frame (27132-27561 vs 33068-33337 with 4 per launch: host-bound) nor the 0.4-4 s C4/C5 frames,
     # whose tails are a small part of them.
+    # Nor for frames of more than one pass launch (C3's 64 passes: 25107 vs 25870 Mrays/s with 8 per launch):
+    # their launches already follow each other on a context.
+    wl = Workload(args.workload)
     group = int(os.environ.get("PT_BENCH_GROUP", "0")) or (
-        1 if heavy or args.workload == "c1" else 4 if world in (2, 3) else 8)
+        1 if heavy or args.workload == "c1" or wl.spp > 8 else 4 if world in (2, 3) else 8)
     inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or (
         2 if group > 1 else 3 if world == 1 else 5)
     grid_share = int(os.environ.get("PT_BENCH_GRID_SHARE", "0")) or (
         (45 if inflight == 3 and not heavy and group == 1 else 100 // (inflight - 1)) if inflight >= 3 else 100)
-    wl = Workload(args.workload)
     scene, cfg, cam = wl.scene, wl.cfg, wl.cam
     width, height, spp = wl.width, wl.height, wl.spp
     rs, frames = [], []
@@ -362,6 +364,7 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    timed_kernel = rs[0].last_kernel()  # the timed launches' kernel (frame groups: the MULTI instance)
     segments = sum(q.stats()["segments"] for q in rs)
     # dominant kernel: the pass kernel (persistent schedule) or the BVH-walk extend kernel (wavefront)
     kind = 0 if schedule == "persistent" else 1
@@ -512,6 +515,7 @@ def main() -> int:
             "frac_lane_weighted": round(valu_lanes / avg_launch_s / 1e9 / valu_peak, 4) if valu_lanes else None,
             "valu_lane_weighted_per_launch": round(valu_lanes) if valu_lanes else None,
             "kernel": kernel_name,
+            "kernel_timed": timed_kernel,
             "counters_from": ("one GPU" if world == 1 else
                               f"rank 0's share of {world}, profiled on its own" if per_rank else
                               f"the 1-GPU frame's profile / {world}"),

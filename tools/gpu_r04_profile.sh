@@ -27,6 +27,7 @@ P="python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/$TAG/pmc_fetch -o run -- $P > gpurun_out/$TAG/pmc_fetch.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/$TAG/pmc_write -o run -- $P > gpurun_out/$TAG/pmc_write.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/$TAG/pmc_sq -o run -- $P > gpurun_out/$TAG/pmc_sq.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d gpurun_out/$TAG/pmc_sq_group8 -o run -- python3 tools/share_render.py --n 1 --frames 2 --group 8 > gpurun_out/$TAG/pmc_sq_group8.log 2>&1 || exit $?
 unset PT_BENCH_INFLIGHT PT_BENCH_GROUP
 timeout -k 10 120 python3 tools/uprof.py metric > gpurun_out/$TAG/uprof_metric.json 2> gpurun_out/$TAG/uprof_metric.err || exit $?
 if [ -d pathtracerwithcuda_amd/lib_dup1 ]; then
