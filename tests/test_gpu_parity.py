@@ -379,6 +379,38 @@ def test_metric_frame_at_the_bench_launch_shape(bench_gpu):
     assert launches == {0: 1, 3: 1}, launches
 
 
+def test_metric_frames_grouped_as_the_bench_times_them(bench_gpu):
+    """bench.py's default timed launch at N = 1: the metric frame rendered by pt_render_frames, several frames
+    per launch (pass_kernel_u's MULTI instance, one accumulate per frame), each through its own camera. Every
+    pixel of every frame against the oracle's frame of that camera: the bench's camera for frames 0 and 2, a
+    turned camera for frame 1, so a refill that spans two frames' units must switch cameras."""
+    import torch
+
+    import bench
+    wl = bench.Workload("metric")
+    r = bench_gpu
+    r.upload(wl.scene, wl.cfg)
+    r.setup_frame(wl.width, wl.height)
+    turned = pt.camera(wl.width, wl.height, yaw=0.35, **BENCH_CAM)
+    cams = [wl.cam, turned, wl.cam]
+    n = wl.width * wl.height * 3
+    imgs = [torch.zeros(n, dtype=torch.float32, device="cuda:0") for _ in cams]
+    imgs8 = [torch.zeros(n, dtype=torch.uint8, device="cuda:0") for _ in cams]
+    r.stats_reset()
+    r.render_frames(cams, wl.cfg, imgs, imgs8, 1, 8, write_u8=2)
+    r.synchronize()
+    assert r.kernel_time_kind(0)[1] == 1, "one pass launch for the three frames"
+    assert "MULTI" in r.last_kernel(), r.last_kernel()
+    refs = {}
+    for f, cam in enumerate(cams):
+        key = id(cam)
+        if key not in refs:
+            refs[key] = oracle.render(wl.scene.view, cam, wl.cfg, 1, 8)
+        ref, ref8, _ = refs[key]
+        assert_bitwise(imgs[f].cpu().numpy().reshape(-1, 3), ref, f"grouped frame {f} float")
+        assert_bitwise(imgs8[f].cpu().numpy().reshape(-1, 3), ref8, f"grouped frame {f} 8-bit")
+
+
 def test_c2_diffuse_mesh_frame(bench_gpu):
     """BASELINE config C2 as its own workload (bench.py --workload c2): the Cornell walls and light with
     the 70k-triangle mesh, diffuse only, no spheres, 1280x720, 8 passes at the bench launch shape. Whole
