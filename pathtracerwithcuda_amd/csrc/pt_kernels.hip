@@ -328,7 +328,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                                                                 int walk_steps, int tri_min, int walk_min) {
     const int lane = threadIdx.x & 63;
     const LaunchParams* P0 = params;
-    const float clamp_hi = (float)P0->cfg.max_depth * 2.0f;
     // workgroup copies in LDS: the first mesh ranges, every material and every sphere (the launch
     // reserves their bytes of dynamic LDS; pass_kernel_u runs only when that fits, PT_LDS_TABLES)
     __shared__ int2 lds_mesh[PT_LDS_MESHES];
@@ -375,7 +374,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     int32_t pseed = 0;
     int depth = 0;
     int mode = LANE_WANT;
-    float wbound = __builtin_inff();  // every mesh walk's starting min_t (medium-bounded mode only)
+    float wbound = __builtin_inff();  // every mesh walk's starting min_t (PT_FEAT_MBOUND instances only)
     unsigned long long segments = 0;  // wave-uniform: lanes shaded (ray segments traced)
     Counters none = {0u, 0u, 0u, 0u, 0u, 0u};
     // the units of one frame copy; a pt_render_frames launch has `frames` copies one after another
@@ -443,7 +442,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                         if (cfg.max_depth > 0) {
                             mode = LANE_NEW;
                         } else {
-                            finish_unit(til, cfg, out, ps, unit, u, first_pass, write_u8, batch_log2, clamp_hi, depth);
+                            finish_unit(til, cfg, out, ps, unit, u, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
                         }
                     }
                 } else if (drained) {
@@ -472,13 +471,13 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 if (cfg.max_depth > 0) {
                     mode = LANE_NEW;
                 } else {
-                    finish_unit(til, cfg, out, ps, unit, lu, first_pass, write_u8, batch_log2, clamp_hi, depth);
+                    finish_unit(til, cfg, out, ps, unit, lu, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
                     mode = LANE_WANT;
                 }
             }
         }
         if (mode == LANE_NEW) {
-            if ((FEAT & PT_FEAT_MEDIUM) && cfg.medium_bound) {
+            if (FEAT & PT_FEAT_MBOUND) {
                 wbound = medium_bound(sc, cfg, ps.medium, depth, pseed);
                 mode = begin_segment(sc, roots, lds_mesh, lds_root, ps, inv, h, w, mesh, wbound);
             } else {
@@ -509,7 +508,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (mode == LANE_READY) {  // the pass's end for this unit, or the next trace step
                 depth++;
                 if (!alive || depth >= cfg.max_depth) {
-                    finish_unit(til, cfg, out, ps, unit, MULTI ? frame_local(unit, frame_units) : unit, first_pass, write_u8, batch_log2, clamp_hi, depth);
+                    finish_unit(til, cfg, out, ps, unit, MULTI ? frame_local(unit, frame_units) : unit, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
                     mode = LANE_WANT;
                 } else {
                     mode = LANE_NEW;  // its next segment starts in the next round's refill, with the new paths
@@ -537,7 +536,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             }
             // the walk state is reset whether or not a mesh is left (a READY lane does not read it), so
             // the branches above only produce a range and the compiler merges no walk fields
-            walk_start(w, range, (FEAT & PT_FEAT_MEDIUM) ? wbound : __builtin_inff());
+            walk_start(w, range, (FEAT & PT_FEAT_MBOUND) ? wbound : __builtin_inff());
             mode = more ? LANE_WALK : LANE_READY;
         };
         // the parked triangle's geometry, loaded at the park; scoped to the walk loop, which no lane leaves
@@ -874,9 +873,11 @@ static PassFn pass_fn(bool leaf1, bool stats, int minw) {
 }
 
 // PT_MIN_WAVES overrides the occupancy target: 8 waves/SIMD for pass_kernel (64 VGPRs); for pass_kernel_u
-// 7 when the scene reaches no participating medium (72 VGPRs: no spills without textures, +3.5 % over 6 on
-// the bench frame; one cold spill with textures, +6.7 % on C5) and 6 otherwise (80 VGPRs; at 72 the medium
-// step spills: C4 5049 vs 5378 Mrays/s, profiles/r02/workloads).
+// 8 when the scene reaches neither textures nor a participating medium (64 VGPRs without spills since round 4
+// recomputes the hit point and the clamp bound where they are used: metric +1.6 % with frame groups, +1.2 %
+// without, C3 +1.1 %, C2 +0.9 %; profiles/r04/knobs/waves_ab2.txt), 7 with textures (72 VGPRs, one cold
+// spill; +6.7 % over 6 on C5) and 6 with a medium (80 VGPRs; 7 fits without spills since round 4 but is slower:
+// C4 5567-5573 vs 5709-5731 Mrays/s, profiles/r04/knobs/waves_ab1.txt).
 int pass_min_waves(bool unified, int feat) {
     static int w = [] {
         const char* e = getenv("PT_MIN_WAVES");
@@ -885,7 +886,12 @@ int pass_min_waves(bool unified, int feat) {
     }();
     if (w) return w;
     if (!unified) return 8;
-    return (feat & PT_FEAT_MEDIUM) ? 6 : 7;
+    // 8 without textures or media (64 VGPRs, no spills since the hit point is recomputed at use: metric +0.8 %
+    // one frame per launch, C3 +1 %); 6 with a medium even where 7 fits without spills (C4 5567-5573 vs
+    // 5709-5731 Mrays/s: more waves only thrash the 51-MB tree's cache lines; profiles/r04/knobs/waves_ab1.txt)
+    static const int plain = env_int("PT_PLAIN_WAVES", 8, 5, 8);
+    static const int medium = env_int("PT_MEDIUM_WAVES", 6, 5, 8);
+    return (feat & PT_FEAT_MBOUND) ? 6 : (feat & PT_FEAT_MEDIUM) ? medium : (feat & PT_FEAT_TEX) ? 7 : plain;
 }
 
 // PT_UNIFIED=0 selects pass_kernel for the default configuration (leaf size 1, uninstrumented);
@@ -905,10 +911,12 @@ using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int,
 static PassFnU pass_fn_u(int minw, int feat, bool multi, int* feat_used, int* minw_used) {
     static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
     static const int prof = env_int("PT_UPROF", 0, 0, 1);
-    if (!spec) feat = PT_FEAT_ALL;
-    if (multi) {
+    if (!spec) feat = PT_FEAT_ALL | (feat & PT_FEAT_MBOUND);
+    if (multi) {  // render_frames fuses frames only without the medium bound
+        feat &= PT_FEAT_ALL;
         *feat_used = feat;
         *minw_used = (feat & PT_FEAT_MEDIUM) ? 6 : 7;
+        if (feat == 0 && minw == 8) { *minw_used = 8; return pass_kernel_u<8, false, 0, true>; }
         switch (feat) {
             case 0: return pass_kernel_u<7, false, 0, true>;
             case 1: return pass_kernel_u<6, false, 1, true>;
@@ -919,17 +927,18 @@ static PassFnU pass_fn_u(int minw, int feat, bool multi, int* feat_used, int* mi
     if (prof) { *feat_used = PT_FEAT_ALL; *minw_used = 6; return pass_kernel_u<6, true, PT_FEAT_ALL>; }
     *feat_used = feat;
     *minw_used = minw;
-#define PT_U_CASE(W, F) case W * 4 + F: return pass_kernel_u<W, false, F>;
-    switch (minw * 4 + feat) {
+#define PT_U_CASE(W, F) case W * 8 + F: return pass_kernel_u<W, false, F>;
+    switch (minw * 8 + feat) {
         PT_U_CASE(5, 0) PT_U_CASE(5, 1) PT_U_CASE(5, 2) PT_U_CASE(5, 3)
-        PT_U_CASE(6, 0) PT_U_CASE(6, 1) PT_U_CASE(6, 2) PT_U_CASE(6, 3)
-        PT_U_CASE(7, 0) PT_U_CASE(7, 1) PT_U_CASE(7, 2) PT_U_CASE(7, 3)
+        PT_U_CASE(6, 0) PT_U_CASE(6, 1) PT_U_CASE(6, 2) PT_U_CASE(6, 3) PT_U_CASE(6, 5) PT_U_CASE(6, 7)
+        PT_U_CASE(7, 0) PT_U_CASE(7, 1) PT_U_CASE(7, 2) PT_U_CASE(7, 3) PT_U_CASE(7, 5) PT_U_CASE(7, 7)
         PT_U_CASE(8, 0) PT_U_CASE(8, 1) PT_U_CASE(8, 2) PT_U_CASE(8, 3)
         default: break;
     }
 #undef PT_U_CASE
-    *feat_used = PT_FEAT_ALL;
+    *feat_used = PT_FEAT_ALL | (feat & PT_FEAT_MBOUND);
     *minw_used = 6;
+    if (feat & PT_FEAT_MBOUND) return pass_kernel_u<6, false, PT_FEAT_ALL | PT_FEAT_MBOUND>;
     return pass_kernel_u<6, false, PT_FEAT_ALL>;
 }
 

@@ -633,6 +633,9 @@ __device__ __forceinline__ float medium_bound(const DevScene& sc, const DevConfi
 #define PT_FEAT_MEDIUM 1
 #define PT_FEAT_TEX 2
 #define PT_FEAT_ALL 3
+// PT_FEAT_MBOUND: the medium-bounded walk is on (pt_set_medium_bound; with PT_FEAT_MEDIUM only). Only these
+// instances hold the walk's starting bound, one more register through the walk.
+#define PT_FEAT_MBOUND 4
 
 // The zero-specular shortcut's per-lane conditions (shade_hit): thr finite, |d|^2 and |n|^2 <= 1 + 2^-12, and
 // the energy bound non-negative. Comparisons are false for NaN, so a NaN anywhere refuses the shortcut.
@@ -706,7 +709,18 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
     // material of the hit (:496-527); fields are read where they are used. The texture modulation
     // (:518-526) is applied in the branch that uses it (specular: reflect, diffuse: diffuse), from the
     // interpolated uv, so only uv stays live through Fresnel and the bounce choice.
-    const v3 point = fma3(d, min_t, o);  // point_on_ray (ray.h:16; sphere.h:50 likewise), contracted
+    // the hit point, point_on_ray (ray.h:16; sphere.h:50 likewise), contracted. Without textures it is computed
+    // where it is used (the sphere normal, the new origin) from o, d and min_t rather than held through the
+    // Fresnel and bounce code: with the clamp bound computed at use (pt_kernels.hip) the bench kernel then fits
+    // 64 VGPRs (8 waves) without spills. The textured kernel keeps it (C5 -0.5 % recomputed,
+    // profiles/r04/knobs/waves_ab1.txt). The same value either way.
+    constexpr bool lazy_point = !(FEAT & PT_FEAT_TEX);
+    v3 held_point;
+    if constexpr (!lazy_point) held_point = fma3(d, min_t, o);
+    auto point = [&]() -> v3 {
+        if constexpr (lazy_point) return fma3(d, min_t, o);
+        else return held_point;
+    };
     v3 normal;
     int mid;
     v2 uv = mk2(0.0f, 0.0f);
@@ -714,7 +728,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
     if (h.type == 1) {
         float4 s = sc.spheres[2 * h.prim];
         mid = f2i(sc.spheres[2 * h.prim + 1].x);
-        normal = normalize(point - mk3(s.x, s.y, s.z));
+        normal = normalize(point() - mk3(s.x, s.y, s.z));
     } else {
         // the hit record's four 16-B loads through a buffer descriptor, issued together: the material id
         // (s3.w) arrives with the normals (a generic pointer here let the compiler merge it with the
@@ -796,7 +810,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
             v3 spec = mk3(M.specular[0], M.specular[1], M.specular[2]);
             if (textured && M.specular_texture_id != -1)
                 spec = spec * sample_texture(sc, M.specular_texture_id, uv, cfg.use_bilinear);
-            ps->o = point + bias_v;
+            ps->o = point() + bias_v;
             ps->d = mr;
             ps->thr = ps->thr * (spec * shadow);
         } else {        // diffuse (:597-610)
@@ -805,11 +819,11 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const DevConfig& c
                 diff = diff * sample_texture(sc, M.diffuse_texture_id, uv, cfg.use_bilinear);
             ps->rad = fma3v(ps->thr, mk3(M.emission[0], M.emission[1], M.emission[2]), ps->rad);  // +=, contracted
             ps->thr = ps->thr * diff;
-            ps->o = point + bias_v;
+            ps->o = point() + bias_v;
             ps->d = dir;
         }
     } else {  // refraction (:585-596)
-        ps->o = point - bias_v;
+        ps->o = point() - bias_v;
         ps->d = refr;
         ps->medium = out_medium;
         ps->thr = ps->thr * (ratio_oi * ratio_oi);  // ratio = out_n / in_n

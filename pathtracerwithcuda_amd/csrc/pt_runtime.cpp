@@ -493,7 +493,7 @@ struct pt_context {
     unsigned int* band_cost = nullptr;
     int band_cost_n = 0;
     bool band_cost_on = false;
-    int grid[2][2][4] = {};
+    int grid[2][2][8] = {};
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
     size_t ev_used = 0;
@@ -817,12 +817,16 @@ int pass_lds_bytes(const pt_context* ctx) {
     return ctx->material_num * (int)sizeof(DevMaterial) + ctx->scene.sphere_num * 32;
 }
 
+int env_medium_bound();
+
 // The features a render can reach: the scene's, plus a participating medium when the configured air
-// scatters or absorbs (shade_hit's medium step runs for air paths then).
+// scatters or absorbs (shade_hit's medium step runs for air paths then), plus the medium-bounded walk
+// (pt_set_medium_bound) where there is a medium to bound.
 int render_feat(const pt_context* ctx, const DevConfig& dc) {
     int f = ctx->scene_feat;
     for (int c = 0; c < 3; c++)
         if (dc.air_absorption[c] != 0.0f || dc.air_reduced_scattering[c] != 0.0f) f |= PT_FEAT_MEDIUM;
+    if ((f & PT_FEAT_MEDIUM) && (ctx->medium_bound >= 0 ? ctx->medium_bound : env_medium_bound())) f |= PT_FEAT_MBOUND;
     return f;
 }
 
@@ -838,7 +842,7 @@ PassChoice pass_choice(const pt_context* ctx, int feat) {
 
 int pass_grid(pt_context* ctx, int feat) {
     const PassChoice pc = pass_choice(ctx, feat);
-    int& g = ctx->grid[pc.leaf1 ? 1 : 0][pc.stats ? 1 : 0][feat & 3];
+    int& g = ctx->grid[pc.leaf1 ? 1 : 0][pc.stats ? 1 : 0][feat & 7];
     if (g == 0) {
         g = pass_grid_size(pc, pass_lds_bytes(ctx));
         // PT_GRID_PCT: experiment knob, a percentage of the occupancy-sized grid
@@ -1105,7 +1109,8 @@ int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, con
         if ((int)cams[f].resolution.x != ctx->width) { set_error("camera width != frame width"); return PT_E_ARG; }
     const int feat = render_feat(ctx, lp.cfg);
     PassChoice pc = pass_choice(ctx, feat);
-    const bool fused = frames > 1 && !wavefront_schedule(ctx) && pass_uses_unified(pc, pass_lds_bytes(ctx));
+    const bool fused = frames > 1 && !wavefront_schedule(ctx) && pass_uses_unified(pc, pass_lds_bytes(ctx)) &&
+                       !(feat & PT_FEAT_MBOUND);
     pc.multi = fused;
     if (!fused) {
         float* const img0 = ctx->image;
