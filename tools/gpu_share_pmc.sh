@@ -3,11 +3,11 @@
 # roofline. Only gpurun_out/ comes back from the GPU box, so the summary is written there too; record
 # it here afterwards with
 #   python3 tools/traffic_summary.py gpurun_out/share<N> profiles/<round>/share<N> \
-#       --workload "<workload key>/tiled<N>" --kernel "pass_kernel_u<7, false, 0>" --round <round>
+#       --workload "<workload key>/tiled<N>" --kernel "pass_kernel_u<8, false, 0, false>" --round <round>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-K="pass_kernel_u<7, false, 0>"
+K="pass_kernel_u<8, false, 0, false>"
 for N in ${COUNTS:-2 4 8}; do
   D=gpurun_out/share$N
   mkdir -p $D

@@ -20,7 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("dup")
 ap.add_argument("uprof")
 ap.add_argument("--workload", default=None)
-ap.add_argument("--kernel", default="pass_kernel_u<7, false, 0")
+ap.add_argument("--kernel", default="pass_kernel_u<8, false, 0, false>")
 args = ap.parse_args()
 
 
