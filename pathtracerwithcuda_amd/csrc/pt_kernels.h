@@ -24,7 +24,10 @@ struct PassChoice {
     int feat;
     bool il;  // the inline-leaf copy of the node array exists (every leaf's skip index is the next record)
     bool multi = false;  // a pt_render_frames launch (several frames): pass_kernel_u's MULTI instance
+    bool small = false;  // a launch of fewer than PT_SMALL_LAUNCH units (pass_min_waves)
 };
+// Launches of fewer units than this run the plain kernel at 7 waves instead of 8 (pass_min_waves).
+#define PT_SMALL_LAUNCH (1ll << 21)
 // whether launch_pass runs pass_kernel_u for this choice (its node array may then be the inline-leaf copy)
 bool pass_uses_unified(const PassChoice& pc, int lds_bytes);
 // inline-leaf copy of the node array for pass_kernel_u (pt_kernels.hip inline_leaves_kernel)

@@ -878,7 +878,7 @@ static PassFn pass_fn(bool leaf1, bool stats, int minw) {
 // without, C3 +1.1 %, C2 +0.9 %; profiles/r04/knobs/waves_ab2.txt), 7 with textures (72 VGPRs, one cold
 // spill; +6.7 % over 6 on C5) and 6 with a medium (80 VGPRs; 7 fits without spills since round 4 but is slower:
 // C4 5567-5573 vs 5709-5731 Mrays/s, profiles/r04/knobs/waves_ab1.txt).
-int pass_min_waves(bool unified, int feat) {
+int pass_min_waves(bool unified, int feat, bool small) {
     static int w = [] {
         const char* e = getenv("PT_MIN_WAVES");
         int v = e ? atoi(e) : 0;
@@ -891,7 +891,10 @@ int pass_min_waves(bool unified, int feat) {
     // 5709-5731 Mrays/s: more waves only thrash the 51-MB tree's cache lines; profiles/r04/knobs/waves_ab1.txt)
     static const int plain = env_int("PT_PLAIN_WAVES", 8, 5, 8);
     static const int medium = env_int("PT_MEDIUM_WAVES", 6, 5, 8);
-    return (feat & PT_FEAT_MBOUND) ? 6 : (feat & PT_FEAT_MEDIUM) ? medium : (feat & PT_FEAT_TEX) ? 7 : plain;
+    // a small launch (C1's 512x512x4 units: 128 per wave at 8 waves) is mostly its waves' first chunks and
+    // tails: 7 waves (C1 33129-34058 vs 30978-31236 Mrays/s at 8, profiles/r04/knobs/c1_waves.txt)
+    return (feat & PT_FEAT_MBOUND) ? 6 : (feat & PT_FEAT_MEDIUM) ? medium : (feat & PT_FEAT_TEX) ? 7
+                                                                                : small ? (plain < 7 ? plain : 7) : plain;
 }
 
 // PT_UNIFIED=0 selects pass_kernel for the default configuration (leaf size 1, uninstrumented);
@@ -1010,7 +1013,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
         static const int tri_min = env_int("PT_TRI_MIN", 4, 1, 64);
         static const int walk_min = env_int("PT_WALK_MIN", 8, 0, 64);
         int fu, wu;
-        const PassFnU fn = pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, pc.multi, &fu, &wu);
+        const PassFnU fn = pass_fn_u(pass_min_waves(true, pc.feat, pc.small), pc.feat, pc.multi, &fu, &wu);
         const LaunchParams* a0 = params_dev;
         int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2, a5 = shade_min, a6 = walk_steps, a7 = tri_min,
             a8 = walk_min;
@@ -1019,7 +1022,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
         if (e != hipSuccess) return e;
         return hipGetLastError();
     }
-    PassFn fn = pass_fn(pc.leaf1, pc.stats, pass_min_waves(false, pc.feat));
+    PassFn fn = pass_fn(pc.leaf1, pc.stats, pass_min_waves(false, pc.feat, pc.small));
     const LaunchParams* a0 = params_dev;
     static const int chunk = env_int("PT_CHUNK_MEGA", 32, 0, 4096);
     int a1 = first_pass, a2 = write_u8, a3 = chunk, a4 = batch_log2;
@@ -1051,13 +1054,13 @@ std::string pass_kernel_desc(const PassChoice& pc, int lds_bytes) {
     char buf[160];
     if (use_unified(pc, lds_bytes)) {
         int fu, wu;
-        (void)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, pc.multi, &fu, &wu);
+        (void)pass_fn_u(pass_min_waves(true, pc.feat, pc.small), pc.feat, pc.multi, &fu, &wu);
         static const int prof = env_int("PT_UPROF", 0, 0, 1);
         std::snprintf(buf, sizeof(buf), "pass_kernel_u<MINW=%d,FEAT=%d%s>", wu, fu,
                       pc.multi ? ",MULTI" : prof ? ",PROF" : "");
     } else {
         std::snprintf(buf, sizeof(buf), "pass_kernel<LEAF1=%d,STATS=%d,MINW=%d>", pc.leaf1 ? 1 : 0, pc.stats ? 1 : 0,
-                      pass_min_waves(false, pc.feat));
+                      pass_min_waves(false, pc.feat, pc.small));
     }
     return buf;
 }
@@ -1069,8 +1072,8 @@ int pass_grid_size(const PassChoice& pc, int lds_bytes) {
     if (cus <= 0) cus = 256;
     const bool u = use_unified(pc, lds_bytes);
     int fu, wu;
-    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true, pc.feat), pc.feat, pc.multi, &fu, &wu)
-                       : (const void*)pass_fn(pc.leaf1, pc.stats, pass_min_waves(false, pc.feat));
+    const void* fn = u ? (const void*)pass_fn_u(pass_min_waves(true, pc.feat, pc.small), pc.feat, pc.multi, &fu, &wu)
+                       : (const void*)pass_fn(pc.leaf1, pc.stats, pass_min_waves(false, pc.feat, pc.small));
     const size_t lds = u ? (size_t)lds_bytes : 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, u ? PT_UBLOCK : PT_BLOCK, lds) != hipSuccess || blocks <= 0)
         blocks = u ? 4 * PT_BLOCK / PT_UBLOCK : 4;

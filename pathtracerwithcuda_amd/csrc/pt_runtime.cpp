@@ -493,7 +493,7 @@ struct pt_context {
     unsigned int* band_cost = nullptr;
     int band_cost_n = 0;
     bool band_cost_on = false;
-    int grid[2][2][8] = {};
+    int grid[2][2][8][2] = {};
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
     size_t ev_used = 0;
@@ -840,9 +840,11 @@ PassChoice pass_choice(const pt_context* ctx, int feat) {
     return pc;
 }
 
-int pass_grid(pt_context* ctx, int feat) {
-    const PassChoice pc = pass_choice(ctx, feat);
-    int& g = ctx->grid[pc.leaf1 ? 1 : 0][pc.stats ? 1 : 0][feat & 7];
+// small: a launch of fewer than PT_SMALL_LAUNCH units (its kernel may run fewer waves, pass_min_waves)
+int pass_grid(pt_context* ctx, int feat, bool small = false) {
+    PassChoice pc = pass_choice(ctx, feat);
+    pc.small = small;
+    int& g = ctx->grid[pc.leaf1 ? 1 : 0][pc.stats ? 1 : 0][feat & 7][small ? 1 : 0];
     if (g == 0) {
         g = pass_grid_size(pc, pass_lds_bytes(ctx));
         // PT_GRID_PCT: experiment knob, a percentage of the occupancy-sized grid
@@ -1043,9 +1045,7 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     // Single-kernel schedule: up to max_pass_batch() passes per launch (pt_kernels.hip pass_kernel),
     // a power of two so a unit splits into (pixel, pass) by shift and mask.
     const int feat = render_feat(ctx, dc);
-    const int grid = pass_grid(ctx, feat);
-    const PassChoice pc = pass_choice(ctx, feat);
-    ctx->last_kernel = pass_kernel_desc(pc, pass_lds_bytes(ctx));
+    const PassChoice pc0 = pass_choice(ctx, feat);
     const int units = ctx->tiling.unit_count;
     int most = 1;
     while (most * 2 <= max_pass_batch() && (long long)units * most * 2 <= (1ll << 28)) most *= 2;
@@ -1068,7 +1068,10 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
         while (b * 2 <= most && i + b * 2 <= pass_count) { b *= 2; lg++; }
         const int first = first_pass + i;
         const int last = i + b == pass_count;
-        const int g = shared_grid(ctx, grid);
+        PassChoice pc = pc0;
+        pc.small = ((long long)units << lg) < PT_SMALL_LAUNCH;
+        ctx->last_kernel = pass_kernel_desc(pc, pass_lds_bytes(ctx));
+        const int g = shared_grid(ctx, pass_grid(ctx, feat, pc.small));
         const int w8 = write_u8 == 1 || (write_u8 == 2 && last);
         PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
         int rc = ev_begin(ctx, 0);
@@ -1137,8 +1140,6 @@ int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, con
     std::vector<DevCamera> dc((size_t)frames);
     for (int f = 0; f < frames; f++) dc[(size_t)f] = to_dev(cams[f]);
     PT_HIP(hipMemcpyAsync(ctx->cams, dc.data(), dc.size() * sizeof(DevCamera), hipMemcpyHostToDevice, ctx->stream));
-    const int grid = pass_grid(ctx, feat);
-    ctx->last_kernel = pass_kernel_desc(pc, pass_lds_bytes(ctx));
     int most = 1;
     while (most * 2 <= max_pass_batch() && (long long)units * most * 2 * frames <= (1ll << 28)) most *= 2;
     const size_t need = (size_t)units * (size_t)most * (size_t)frames * 12;
@@ -1162,7 +1163,10 @@ int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, con
         PT_HIP(hipMemsetAsync(ctx->fetch, 0, PT_HEAD_SET * sizeof(unsigned int), ctx->stream));
         int rc = ev_begin(ctx, 0);
         if (rc != PT_OK) return rc;
-        PT_HIP(launch_pass(ctx->params, pc, first, lg, w8, shared_grid(ctx, grid), pass_lds_bytes(ctx), ctx->stream));
+        pc.small = (((long long)units * frames) << lg) < PT_SMALL_LAUNCH;
+        ctx->last_kernel = pass_kernel_desc(pc, pass_lds_bytes(ctx));
+        const int g = shared_grid(ctx, pass_grid(ctx, feat, pc.small));
+        PT_HIP(launch_pass(ctx->params, pc, first, lg, w8, g, pass_lds_bytes(ctx), ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;
         for (int f = 0; f < frames; f++)
@@ -1237,7 +1241,8 @@ int abi_render_pass(pt_context* ctx, const pt_render_camera* cam, const pt_confi
         int lg = 0;
         while ((2 << lg) <= B / 2 && ((long long)units << (lg + 1)) <= (1ll << 28)) lg++;
         const int feat = render_feat(ctx, lp.cfg);
-        const PassChoice pc = pass_choice(ctx, feat);
+        PassChoice pc = pass_choice(ctx, feat);
+        pc.small = ((long long)units << lg) < PT_SMALL_LAUNCH;
         ctx->last_kernel = pass_kernel_desc(pc, pass_lds_bytes(ctx));
         const size_t need = (size_t)units * ((size_t)1 << lg) * 12;
         for (int k = 0; k < 2; k++) {
@@ -1258,7 +1263,7 @@ int abi_render_pass(pt_context* ctx, const pt_render_camera* cam, const pt_confi
             if ((rc = ev_begin(ctx, 0)) != PT_OK) return rc;
             // the second slot leaves an eighth of the workgroup slots free: the calls it overlaps launch their
             // accumulates meanwhile, which would otherwise wait for its persistent workgroups to end
-            const int g = pass_grid(ctx, feat);
+            const int g = pass_grid(ctx, feat, pc.small);
             PT_HIP(launch_pass(ctx->spec_params[k], pc, first, lg, 0, k == 0 ? g : std::max(1, g - g / 8),
                                pass_lds_bytes(ctx), ctx->stream));
             if ((rc = ev_end(ctx)) != PT_OK) return rc;
