@@ -293,8 +293,11 @@ def main() -> int:
     # Nor for frames of more than one pass launch (C3's 64 passes: 25107 vs 25870 Mrays/s with 8 per launch):
     # their launches already follow each other on a context.
     wl = Workload(args.workload)
+    # At 8 waves (profiles/r04/group/group_size_n2_n4.txt) 8 per launch beats 4 at N = 2 too (2.595-2.605 vs
+    # 2.653-2.659 ms per frame); 10 per launch is 1-3 % faster still at N = 2 and 4 over a 20-frame run (two
+    # launches of 10), but that is the driver's step count, not a property of the renderer: 8 everywhere.
     group = int(os.environ.get("PT_BENCH_GROUP", "0")) or (
-        1 if heavy or args.workload == "c1" or wl.spp > 8 else 4 if world in (2, 3) else 8)
+        1 if heavy or args.workload == "c1" or wl.spp > 8 else 8)
     inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or (
         2 if group > 1 else 3 if world == 1 else 5)
     grid_share = int(os.environ.get("PT_BENCH_GRID_SHARE", "0")) or (

@@ -16,8 +16,8 @@ run() {  # name ranks port extra-env...
   python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], 'ranks: image_matches_1gpu', d['config']['image_matches_1gpu'], 'frames per launch', d['config']['frames_per_launch'], d['value'], 'Mrays/s')" gpurun_out/$TAG/$m.json $n
   cmp gpurun_out/$TAG/n1.png gpurun_out/$TAG/$m.png || exit 4
 }
-# b*: one frame per launch (PT_BENCH_GROUP=1); g*: the default frame groups at N > 1 (4 frames per launch at
-# 2-3 ranks, 8 at 4+, one collective per group): 5 steps = one launch of 4 frames and one of 1, or one of 5
+# b*: one frame per launch (PT_BENCH_GROUP=1); g*: the default frame groups at N > 1 (8 frames per launch,
+# one collective per group): 5 steps = one launch of 5 frames
 run b2 2 29533 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=1
 run b3 3 29534 PT_FRAME_COLLECTIVE=reduce PT_BENCH_GROUP=1
 run b4 4 29535 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=1
