@@ -57,6 +57,46 @@ def extend_bytes(counts: dict, sphere_count: int) -> float:
     return (24.0 + 16.0 + 16.0 * sphere_count) * seg + 32.0 * counts["nodes"] + 40.0 * counts["tris"]
 
 
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def asset_root() -> str:
+    """A reference-style working directory (res/configuration, res/scene, res/obj, res/texture) holding the
+    scene fixtures of tests/golden/res and the reference's own meshes, textures and lobby skybox from
+    tests/golden/ref_assets.tar.xz (tools/pack_ref_assets.py), unpacked once per pack into the temp
+    directory. /root/reference is not read: it does not exist on the GPU box."""
+    import hashlib
+    import shutil
+    import tarfile
+    import tempfile
+
+    pack = os.path.join(GOLDEN, "ref_assets.tar.xz")
+    digest = hashlib.sha256(open(pack, "rb").read()).hexdigest()[:16]
+    fixtures = hashlib.sha256()
+    for d, _, fs in sorted(os.walk(os.path.join(GOLDEN, "res"))):
+        for f in sorted(fs):
+            fixtures.update(os.path.relpath(os.path.join(d, f), GOLDEN).encode())
+            fixtures.update(open(os.path.join(d, f), "rb").read())
+    root = os.path.join(tempfile.gettempdir(), f"pt_assets_{digest}_{fixtures.hexdigest()[:12]}")
+    if not os.path.isdir(os.path.join(root, "res")):
+        tmp = f"{root}.tmp{os.getpid()}"
+        shutil.rmtree(tmp, ignore_errors=True)
+        shutil.copytree(os.path.join(GOLDEN, "res"), os.path.join(tmp, "res"))
+        with tarfile.open(pack, "r:xz") as tar:
+            for m in tar.getmembers():  # plain files under res/ only
+                if not m.isfile() or not m.name.startswith("res/") or ".." in m.name.split("/"):
+                    raise RuntimeError(f"unexpected member {m.name!r} in {pack}")
+                tar.extract(m, tmp)
+        for d, _, fs in os.walk(tmp):
+            for f in fs:
+                os.chmod(os.path.join(d, f), 0o644)
+        try:
+            os.rename(tmp, root)
+        except OSError:  # another process unpacked it first
+            shutil.rmtree(tmp, ignore_errors=True)
+    return root
+
+
 def procedural_texture(w: int, h: int, seed: int) -> np.ndarray:
     """RGBA8 texture (top row first): checker tiles with per-tile colour noise."""
     rng = np.random.default_rng(seed)
@@ -123,33 +163,26 @@ class Workload:
             self.desc = (f"Cornell box + {self.scene.triangle_count - 22}-triangle torus knot (dragon stand-in) "
                          "with DragonGreen subsurface scattering (sigma_a (40,3,14), sigma_s' 400)")
             self.data = "synthetic: procedural 800k-triangle torus knot + procedural 512^2 cube map"
-        elif name == "c5":  # multi-mesh, diffuse + specular texture maps, 4K
+        elif name == "c5":  # multi-mesh, diffuse + specular texture maps, 4K (SURVEY.md §8(d) C5)
             self.width, self.height, self.spp, self.depth = 3840, 2160, 1024, 12
-            sc = pt.Scene()
-            walls = [sc.add_material(m) for m in ("wall_white", "wall_green", "wall_red", "wall_white", "wall_white")]
-            sc.add_mesh(pt.cornell_shapes(), walls, position=(0.0, -0.8, 1.0), scale=(0.1, 0.1, 0.3))
-            sc.add_mesh([pt.cube_shape()], [sc.add_material("light")], position=(0.0, 3.1, 0.0),
-                        scale=(0.85, 0.05, 0.85))
-            for k, (pos, rot, base) in enumerate([((-1.3, 0.6, -0.8), (0, 30, 0), "red"),
-                                                  ((1.2, 0.6, -0.6), (20, -20, 0), "green"),
-                                                  ((0.0, 1.9, -1.6), (70, 0, 0), "gold")]):
-                td = sc.add_texture(procedural_texture(512, 256, 10 + k))
-                ts = sc.add_texture(procedural_texture(256, 256, 20 + k))
-                m = sc.add_material(pt.material(base, diffuse_texture_id=td, specular_texture_id=ts))
-                sc.add_mesh([pt.torus_knot(300, 60, uv_repeat=6.0)], [m], position=pos, scale=(0.45, 0.45, 0.45),
-                            rotate=rot)
-            tc = sc.add_texture(procedural_texture(1024, 1024, 30))
-            mc = sc.add_material(pt.material("diffuse_white", diffuse_texture_id=tc, specular_texture_id=tc))
-            sc.add_mesh([pt.cube_shape()], [mc], position=(0.0, 0.0, 0.6), scale=(0.6, 0.6, 0.6), rotate=(0, 35, 0))
-            sc.set_cube_map(pt.procedural_cube_map(512))
-            self.scene = sc.build()
-            self.key = "c5_textured_multimesh_3840x2160_spp1024_d12"
-            self.desc = (f"Cornell box + three textured torus knots + a textured cube, {self.scene.triangle_count} "
-                         "triangles, diffuse and specular RGBA8 maps")
-            self.data = "synthetic: procedural meshes and textures + procedural 512^2 cube map"
+            # tests/golden/res/scene/c5_vanille_gallery.json, loaded by the reference-format scene parser from the
+            # reference's own assets: two vanille.obj (25,786 triangles, 15 shapes, vanille.json's per-shape
+            # materials and its five TGA diffuse maps, 256^2-1024^2) + human, cow, monkey, cup, with sponza
+            # *_spec.tga specular maps (512^2 RGBA, 512^2 RGB, 1024^2 RGB), in the Cornell walls under the
+            # cube light, lobby skybox
+            root = asset_root()
+            cfg = pt.configuration(max_tracer_depth=self.depth)
+            self.scene = pt.load_scene(os.path.join(root, "res", "scene", "c5_vanille_gallery.json"), root_dir=root,
+                                       config=cfg)
+            cam_kw = dict(pitch=0.1, radius=9.0, center=(0.0, 0.9, 0.0))  # the room's front opening
+            self.key = "c5_vanille_gallery_3840x2160_spp1024_d12"
+            self.desc = (f"two vanille.obj + human/cow/monkey/cup in the Cornell walls, {self.scene.triangle_count} "
+                         "triangles, vanille TGA diffuse maps + sponza *_spec.tga specular maps, lobby skybox")
+            self.data = "the reference's own meshes, TGA maps and lobby skybox (tests/golden/ref_assets.tar.xz)"
         else:
             raise SystemExit(f"unknown workload {name!r}")
         self.cfg = pt.configuration(max_tracer_depth=self.depth)
+        self.cam_kw = cam_kw
         self.cam = pt.camera(self.width, self.height, **cam_kw)
 
 
@@ -226,6 +259,13 @@ def main() -> int:
     ap.add_argument("--workload", choices=["metric", "c1", "c2", "c3", "c4", "c5"], default="metric",
                     help="metric: BASELINE.json's metric configuration (default); c1: its CPU-path plumbing config "
                          "(the line then carries that frame's CPU-path time as cpu_baseline); c2-c5: its other configs")
+    ap.add_argument("--orbit", type=float, default=0.0, metavar="RAD",
+                    help="advance the camera's yaw by RAD per frame (an interactive caller's moving camera); every "
+                         "frame then has its own camera, 0 (default) keeps one camera for all frames")
+    ap.add_argument("--rccl", action="store_true",
+                    help="at N = 1: run the multi-GPU path anyway, through a one-rank RCCL (torch 'nccl') group: "
+                         "bands = 1, the frame's gather / reduce, barrier and all-reduce on RCCL, and the "
+                         "image_matches_1gpu self-check")
     args = ap.parse_args()
     heavy = args.workload in ("c4", "c5")
     if args.steps is None:
@@ -248,7 +288,7 @@ def main() -> int:
     # so the value is set here, not defaulted (PT_BENCH_HW_QUEUES overrides it; at most 32 on this pool).
     # Tiled (N > 1): 16, so RCCL's own streams get queues of their own beside the five renderer streams
     # instead of queueing behind a persistent pass launch (16 and 8 measured equal for the share itself)
-    hw_queues = os.environ.get("PT_BENCH_HW_QUEUES", "16" if world > 1 else "8")
+    hw_queues = os.environ.get("PT_BENCH_HW_QUEUES", "16" if world > 1 or args.rccl else "8")
     os.environ["GPU_MAX_HW_QUEUES"] = hw_queues
     # Tiled shares batch triangle tests from 3 parked lanes instead of 6: a small share spends most of its
     # launch in the tail, where few lanes walk (8-way share 0.869-0.871 vs 0.887-0.897 ms; at N = 1 it is
@@ -265,9 +305,17 @@ def main() -> int:
     backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
     if os.environ.get("PT_BENCH_SHARE_GPU"):
         local = 0
-    if world > 1:
+    # the multi-GPU code path: every N > 1 run, and N = 1 with --rccl (a one-rank group in this process)
+    distributed = world > 1 or args.rccl
+    if distributed:
         torch.cuda.set_device(local)
-        if backend == "nccl":
+        if world == 1 and "MASTER_ADDR" not in os.environ:  # --rccl run directly: a one-rank group in-process
+            store = dist.HashStore()
+            if backend == "nccl":
+                dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(backend, store=store, rank=0, world_size=1)
+        elif backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
@@ -314,11 +362,11 @@ def main() -> int:
         q.upload(scene, cfg)
         rs.append(q)
         if group > 1:
-            frames.append(pt.FrameGroup(q, width, height, group, dist if world > 1 else None, BAND_ROWS,
+            frames.append(pt.FrameGroup(q, width, height, group, dist if distributed else None, BAND_ROWS,
                                         device=f"cuda:{local}"))
         else:
-            frames.append(pt.TiledFrame(q, width, height, dist if world > 1 else None, BAND_ROWS,
-                                        device=f"cuda:{local}" if world > 1 else None))
+            frames.append(pt.TiledFrame(q, width, height, dist if distributed else None, BAND_ROWS,
+                                        device=f"cuda:{local}" if distributed else None))
     r = rs[0]
     schedule = r.schedule()
 
@@ -335,38 +383,76 @@ def main() -> int:
     # PT_BENCH_LAST_FULL: how many frames at the end of a batch take the whole grid (default 1)
     last_full = int(os.environ.get("PT_BENCH_LAST_FULL", "1"))
 
+    # --orbit: frame i of the run (warm-up frames first) is seen from the bench camera turned by i * RAD of yaw,
+    # as an interactive caller's camera moves between frames; without it every frame shares the one camera
+    def camera_of(i: int):
+        if not args.orbit:
+            return cam
+        return pt.camera(width, height, yaw=float(i) * args.orbit, **wl.cam_kw)
+
+    frame_no = 0  # frames issued so far (warm-up included): the camera index
+    last_launch = None  # (context index, cameras) of the most recent launch
+
     def run(k: int) -> None:
         # the last launch of a batch has no launch behind it to fill the CUs it leaves: it takes the whole
         # grid (every frame is still rendered completely, in order, on its own context). With frame groups a
         # launch takes the next min(G, frames left) frames.
-        nonlocal nframe
+        nonlocal nframe, frame_no, last_launch
         launches = [min(group, k - i) for i in range(0, k, group)]
         for j, n in enumerate(launches):
             q = frames[nframe % inflight]
             full = grid_share < 100 and j >= len(launches) - last_full
             if full:
                 rs[nframe % inflight].set_grid_share(100)
+            cams = [camera_of(frame_no + f) for f in range(n)]
             if group > 1:
-                q.launch([cam] * n, cfg, spp)
+                q.launch(cams, cfg, spp)
             else:
-                q.launch(cam, cfg, spp)
+                q.launch(cams[0], cfg, spp)
             if full:
                 rs[nframe % inflight].set_grid_share(grid_share)
+            last_launch = (nframe % inflight, cams)
             nframe += 1
+            frame_no += n
 
     run(args.warmup)
     torch.cuda.synchronize()
     for q in rs:
         q.stats_reset()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(args.steps)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+
+    # The distributed path must produce the 1-GPU frame. Outside the timed region, rank 0 takes the last TIMED
+    # launch's first and last frame (with frame groups: the MULTI kernel's frames, as every timed frame is made)
+    # and renders each again alone on a fresh untiled context over the whole grid, through the same camera, and
+    # compares them bitwise (float running sum and 8-bit image); the line carries config.image_matches_1gpu and a
+    # mismatch exits 3
+    matches_1gpu = None
+    if distributed and rank == 0:
+        ctx, cams = last_launch
+        picks = sorted({0, len(cams) - 1})
+        got = [frames[ctx].download(f) if group > 1 else frames[ctx].download() for f in picks]
+        solo = pt.Renderer(local)
+        try:
+            if args.medium_bound:
+                solo.set_medium_bound(True)
+            solo.upload(scene, cfg)
+            solo.setup_frame(width, height)
+            matches_1gpu = True
+            for f, (tiled, tiled8) in zip(picks, got):
+                solo.render(cams[f], cfg, 1, spp, write_u8=2)
+                one, one8 = solo.download()
+                matches_1gpu &= bool(np.array_equal(tiled.view(np.uint32).reshape(-1), one.view(np.uint32).reshape(-1))
+                                     and np.array_equal(tiled8.reshape(-1), one8.reshape(-1)))
+        finally:
+            solo.close()
     timed_kernel = rs[0].last_kernel()  # the timed launches' kernel (frame groups: the MULTI instance)
     segments = sum(q.stats()["segments"] for q in rs)
     # dominant kernel: the pass kernel (persistent schedule) or the BVH-walk extend kernel (wavefront)
@@ -379,35 +465,17 @@ def main() -> int:
     lat_frames = max(3, min(5, args.steps))
     r.set_grid_share(100)
     r.stats_reset()
-    if world > 1:
+    if distributed:
         dist.barrier()
     t1 = time.perf_counter()
     for _ in range(lat_frames):
         frames[0].render(cam, cfg, spp)
-    if world > 1:
+    if distributed:
         dist.barrier()
     latency = (time.perf_counter() - t1) / max(lat_frames, 1)
     solo_ms, solo_launches = r.kernel_time_kind(kind)
 
-    # N > 1: the tiled frame must be the 1-GPU frame. Outside the timed region, rank 0 renders the same frame
-    # alone on a fresh untiled context over the whole grid and compares it bitwise (float running sum and 8-bit
-    # image) with the frame its tiled context just gathered (the last frame of the latency loop above)
-    matches_1gpu = None
-    if world > 1 and rank == 0:
-        tiled, tiled8 = frames[0].download()
-        solo = pt.Renderer(local)
-        try:
-            if args.medium_bound:
-                solo.set_medium_bound(True)
-            solo.upload(scene, cfg)
-            solo.setup_frame(width, height)
-            solo.render(cam, cfg, 1, spp, write_u8=2)
-            one, one8 = solo.download()
-        finally:
-            solo.close()
-        matches_1gpu = bool(np.array_equal(tiled.view(np.uint32), one.view(np.uint32)) and np.array_equal(tiled8, one8))
-
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -419,14 +487,15 @@ def main() -> int:
         counts = {k: int(v) for k, v in zip(sorted(counts), c.tolist())}
 
     if rank != 0:
-        if world > 1:
+        if distributed:
             dist.destroy_process_group()
         return 0
 
-    if args.save_image:
+    if args.save_image:  # the last timed launch's first frame (the frame the self-check compares)
         from pathtracerwithcuda_amd.imageio import write_png
-        _, img8 = frames[0].download()
-        write_png(args.save_image, img8)
+        ctx, _ = last_launch
+        _, img8 = frames[ctx].download(0) if group > 1 else frames[ctx].download()
+        write_png(args.save_image, np.asarray(img8).reshape(height, width, 3))
 
     value = segments / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1000.0
@@ -463,9 +532,21 @@ def main() -> int:
     # / the launch's duration measured here with HIP events on the renderer's stream, one frame in flight.
     valu_peak = SIMDS * CLOCK_HZ / 2.0 / 1e9  # G wave-instructions / s
     valu_achieved = valu_insts / avg_launch_s / 1e9 if valu_insts else None
-    # The same instructions over the timed mode's own clock: VALU per frame / ms_per_step (frames in flight
-    # overlap, so this is what the timed figure implies per GPU; it can never exceed 1)
-    valu_timed = valu_insts * frame_launches / (ms_per_step / 1000.0) / 1e9 if valu_insts else None
+    # The same roofline over the timed mode's own clock: the TIMED kernel's VALU per frame / ms_per_step (frames in
+    # flight overlap, so this is what the timed figure implies per GPU). With frame groups the timed launches run
+    # the MULTI instance, which issues fewer instructions per frame than the solo launch (it shares one drain among
+    # its frames): its own count is profiled separately (profiles/traffic.json valu_insts_per_frame_timed, a
+    # --pmc SQ_INSTS_VALU pass over an 8-frame launch) and used here; without that record the field stays null.
+    if group > 1:
+        vt = prof.get("valu_insts_per_frame_timed")
+        valu_timed_frame = float(vt) * scale if vt else None
+    else:
+        valu_timed_frame = valu_insts * frame_launches if valu_insts else None
+    valu_timed = valu_timed_frame / (ms_per_step / 1000.0) / 1e9 if valu_timed_frame else None
+    # the solo launch's duration as rocprofv3's kernel trace averages it (recorded with the counters): the same
+    # fraction priced on the profiler's clock instead of this run's HIP events
+    rp_ms = prof.get("rocprof_avg_launch_ms")
+    valu_rocprof = valu_insts / (float(rp_ms) / 1000.0) / 1e9 if (valu_insts and rp_ms and world == 1) else None
     # Lane-weighted: a wave-instruction counts active lanes / 64 (PT_UPROF lanes per phase x the PT_DUP VALU
     # split per phase, tools/lane_weighted.py, recorded in profiles/traffic.json)
     valu_lanes = float(prof["valu_lane_weighted_per_launch"]) * scale if prof.get("valu_lane_weighted_per_launch") else None
@@ -492,7 +573,7 @@ def main() -> int:
             "workload": workload,
             "scene": wl.desc,
             "width": width, "height": height, "spp": spp, "max_depth": wl.depth,
-            "parallelism": f"tiled{world}" if world > 1 else "single",
+            "parallelism": f"tiled{world}" if distributed else "single",
             "schedule": schedule,
             "medium_bound": bool(args.medium_bound),
             "band_rows": BAND_ROWS if world > 1 else None,
@@ -504,6 +585,7 @@ def main() -> int:
             "ms_per_frame_latency": round(latency * 1000.0, 3),
             "camera_samples_per_s_M": round(width * height * spp * args.steps / elapsed / 1e6, 3),
             "segments_per_frame": segments // max(args.steps, 1),
+            "orbit_rad_per_frame": args.orbit,
         },
         "roofline": {
             "bound": "valu",
@@ -514,7 +596,10 @@ def main() -> int:
             "traffic": round(traffic) if traffic is not None else None,
             "hbm": hbm,
             "valu_insts_per_launch": round(valu_insts) if valu_insts else None,
+            "frac_rocprof_avg": round(valu_rocprof / valu_peak, 4) if valu_rocprof else None,
+            "rocprof_avg_launch_ms": rp_ms if valu_rocprof else None,
             "frac_timed_mode": round(valu_timed / valu_peak, 4) if valu_timed else None,
+            "valu_insts_per_frame_timed": round(valu_timed_frame) if valu_timed_frame else None,
             "frac_lane_weighted": round(valu_lanes / avg_launch_s / 1e9 / valu_peak, 4) if valu_lanes else None,
             "valu_lane_weighted_per_launch": round(valu_lanes) if valu_lanes else None,
             "kernel": kernel_name,
@@ -533,15 +618,17 @@ def main() -> int:
         },
         "cpu_baseline": None,
     }
-    if world > 1:
+    if distributed:
         line["config"]["image_matches_1gpu"] = matches_1gpu
+        line["config"]["collective"] = {"backend": dist.get_backend(), "world_size": world,
+                                        "frame_collective": os.environ.get("PT_FRAME_COLLECTIVE", "gather")}
     if world == 1 and not args.no_cpu_baseline and args.workload in ("metric", "c1"):
         threads, why = host_threads(args.cpu_threads)
         line["cpu_baseline"] = cpu_baseline(wl, threads)
         line["cpu_baseline"]["cpu"] = platform.processor() or platform.machine()
         line["cpu_baseline"]["threads_from"] = why
     print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
         if not matches_1gpu:
             print("[bench] the tiled frame differs from the 1-GPU frame", file=sys.stderr)

@@ -121,7 +121,9 @@ typedef struct {
 
 /* nan: segments whose kill test saw a NaN throughput length and, as the reference does (NaN <= x is false),
  * kept the path (reported so a test can show that its scene reaches that case) */
-typedef struct { unsigned long long nodes, tris, nan; } or_counts;
+/* nan_flight / inf_flight: free flights (:463-464) whose distance is NaN (a draw of exactly 1.0f over sigma_s' = 0:
+ * -log(1) / 0 = -0 / 0) or +inf (sigma_s' = 0, an absorption-only medium); both never scatter (:466) */
+typedef struct { unsigned long long nodes, tris, nan, nan_flight, inf_flight; } or_counts;
 
 /* the product's medium-bounded walk (PT_MEDIUM_BOUND), set per render from bit 9 of math_mode */
 static int or_medium_bound = 0;
@@ -488,6 +490,8 @@ static void trace(const or_scene* sc, int rng_kind, int seed, int depth, const i
     if (cs.reduced_scattering_coefficient.x > 0.0f || v_len(f3(cs.absorption_coefficient)) > cfg->sss_threshold) {
         float r = draw01(&rng);
         float dist = -m_log(mm, r) / cs.reduced_scattering_coefficient.x;
+        if (dist != dist) cnt->nan_flight++;
+        else if (dist == INFINITY) cnt->inf_flight++;
         if (dist < min_t) {
             sig_add(st, k, 1);  /* scatter inside the medium */
             float r1 = draw01(&rng), r2 = draw01(&rng);
@@ -614,7 +618,8 @@ static void gamma_u8(int mm, const pt_configuration* cfg, const float* img, int 
  * Render passes first_pass .. first_pass+pass_count-1 for `n` pixels: pixel_list[k] (or k when
  * pixel_list is NULL). image (n*3 floats) and image256 (n*3 bytes, may be NULL) are the running
  * sum and 8-bit value of entry k, with the reference's pass_counter semantics. stats[0..3] (may be
- * NULL) receive ray segments, BVH nodes visited, triangle tests and NaN-throughput survivals.
+ * NULL) receive ray segments, BVH nodes visited, triangle tests, NaN-throughput survivals, and free flights with a
+ * NaN / an infinite distance (stats[4], stats[5]).
  * Returns 0 or -1 (alloc).
  */
 int or_render_sig(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangle* triangles, int sphere_num,
@@ -647,7 +652,7 @@ int or_render_sig(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangl
 #else
     (void)threads;
 #endif
-    unsigned long long segs = 0, nodes = 0, tris = 0, nans = 0;
+    unsigned long long segs = 0, nodes = 0, tris = 0, nans = 0, nanf = 0, inff = 0;
     for (int pass = first_pass; pass < first_pass + pass_count; pass++) {
         int seed = pass;
         #pragma omp parallel for schedule(dynamic, 256)
@@ -656,18 +661,22 @@ int or_render_sig(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangl
         for (int depth = 0; depth < cfg->max_tracer_depth; depth++) {
             if (count == 0) break;
             segs += (unsigned long long)count;
-            unsigned long long dn = 0, dt = 0, dnan = 0;
-            #pragma omp parallel for schedule(dynamic, 256) reduction(+ : dn, dt, dnan)
+            unsigned long long dn = 0, dt = 0, dnan = 0, dnf = 0, dif = 0;
+            #pragma omp parallel for schedule(dynamic, 256) reduction(+ : dn, dt, dnan, dnf, dif)
             for (int ai = 0; ai < count; ai++) {
-                or_counts c = {0, 0, 0};
+                or_counts c = {0, 0, 0, 0, 0};
                 trace(&sc, rng_kind, seed, depth, pixel_list, ai, &st, &c);
                 dn += c.nodes;
                 dt += c.tris;
                 dnan += c.nan;
+                dnf += c.nan_flight;
+                dif += c.inf_flight;
             }
             nodes += dn;
             tris += dt;
             nans += dnan;
+            nanf += dnf;
+            inff += dif;
             count = shrink(st.alive, count);
         }
         float hi = (float)cfg->max_tracer_depth * 2.0f;
@@ -684,7 +693,7 @@ int or_render_sig(int mesh_num, pt_bvh_node_device** bvh_nodes, const pt_triangl
             if (sigs) sigs[(size_t)(pass - first_pass) * n + k] = st.sig[k];
         }
     }
-    if (stats) { stats[0] = segs; stats[1] = nodes; stats[2] = tris; stats[3] = nans; }
+    if (stats) { stats[0] = segs; stats[1] = nodes; stats[2] = tris; stats[3] = nans; stats[4] = nanf; stats[5] = inff; }
     free(st.alive); free(st.rays); free(st.thr); free(st.rad); free(st.sca); free(st.sig);
     return 0;
 }

@@ -91,7 +91,7 @@ def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.
         img8 = image256.reshape(n, 3)
     else:
         img8 = np.zeros((n, 3), np.uint8) if with_u8 else None
-    stats = (C.c_ulonglong * 4)()
+    stats = (C.c_ulonglong * 6)()
     sigs = np.zeros((pass_count, n), np.uint64) if signatures else None
     rc = L.or_render_sig(view.mesh_num, C.cast(view.bvh_nodes, C.c_void_p), C.cast(view.triangles, C.c_void_p),
                      view.sphere_num, C.cast(view.spheres, C.c_void_p), C.cast(view.sky_cube_map, C.c_void_p),
@@ -101,7 +101,8 @@ def render(view, cam, cfg, first_pass: int = 1, pass_count: int = 1, pixels: np.
                      sigs.ctypes.data if sigs is not None else None)
     if rc != 0:
         raise MemoryError("oracle allocation failed")
-    st = {"segments": stats[0], "nodes": stats[1], "tris": stats[2], "nan_alive": stats[3]}
+    st = {"segments": stats[0], "nodes": stats[1], "tris": stats[2], "nan_alive": stats[3],
+          "nan_flight": stats[4], "inf_flight": stats[5]}
     if sigs is not None:
         st["signatures"] = sigs
     return img, img8, st
@@ -123,6 +124,32 @@ def rng_stream(kind: str, seed: int, n: int, a: float = 0.0, b: float = 1.0) -> 
 
 def hash_(a: int) -> int:
     return int(lib().or_hash(int(np.int32(a))))
+
+
+def hash_np(a: np.ndarray) -> np.ndarray:
+    """or_hash (path_tracer_kernel.cu:35-44) over an int array: int32 wrap-around, arithmetic >>."""
+    a = np.asarray(a).astype(np.int64).astype(np.uint32)
+    with np.errstate(over="ignore"):
+        a = (a + np.uint32(0x7ed55d16)) + (a << np.uint32(12))
+        a = (a ^ np.uint32(0xc761c23c)) ^ (a.view(np.int32) >> 19).view(np.uint32)
+        a = (a + np.uint32(0x165667b1)) + (a << np.uint32(5))
+        a = (a + np.uint32(0xd3a2646c)) ^ (a << np.uint32(9))
+        a = (a + np.uint32(0xfd7046c5)) + (a << np.uint32(3))
+        a = (a ^ np.uint32(0xb55a4f09)) ^ (a.view(np.int32) >> 16).view(np.uint32)
+    return a.view(np.int32)
+
+
+def trace_first_draws(pass_: int, pixels: np.ndarray, depth: int) -> np.ndarray:
+    """The first uniform(0, 1) draw of trace_ray_kernel's generator for (pass, pixel, depth) — the free-flight
+    draw of a segment in a medium (path_tracer_kernel.cu:415,463): thrust minstd seeded with
+    hash(pass) * hash(pixel) * hash(depth) (int32 wrap), one step, (x - 1) / 2^31 in float32."""
+    hp = hash_np(np.asarray(pixels)).view(np.uint32).astype(np.uint64)
+    k = (int(hash_np(np.array([pass_]))[0]) * int(hash_np(np.array([depth]))[0])) & 0xffffffff
+    s = (hp * np.uint64(k)) & np.uint64(0xffffffff)
+    x0 = s % np.uint64(2147483647)
+    x0[x0 == 0] = 1
+    x1 = (x0 * np.uint64(48271)) % np.uint64(2147483647)
+    return (x1 - 1).astype(np.float32) / np.float32(2147483648.0)
 
 
 def math_eval(which: int, mode: str, x: np.ndarray):

@@ -525,6 +525,10 @@ struct pt_context {
     // the reference ABI's scene check: digest of the caller's raw scene bytes at the last translation
     bool raw_valid = false;
     StageDigest raw{};
+    // the pass_counter of the last reference-ABI call: a call that does not continue it (pass_counter neither 1
+    // nor last + 1: the caller rendered the passes between on its CPU twin, which also sees in-place edits made
+    // since its own pass 1) re-checks the scene before it renders
+    int abi_last_pass = 0;
     // the reference ABI on host-visible images: one-pass launches go through pass_rad (rad_single) and the
     // accumulate launch waits for the caller's running sum, uploaded on copy_stream meanwhile (acc_wait)
     hipStream_t copy_stream = nullptr;
@@ -1870,9 +1874,21 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
     };
     StageDigest rd;
     bool rd_ok = false;
-    if (rc == PT_OK && !same) {  // new pointers: translate before rendering
+    // A continuation pass that does not follow this library's own last pass: the passes in between ran elsewhere
+    // (Core/path_tracer.cpp:46-91 picks the CPU twin per pass, window.cpp:580-588), possibly after an in-place
+    // edit and its pass-1 reset that this library never saw. The caller's bytes are checked BEFORE rendering (a
+    // continuation adds into the running sum, so it cannot be redone as pass 1 is).
+    const bool gap = pass_counter != 1 && pass_counter != ctx->abi_last_pass + 1;
+    if (rc == PT_OK && same && gap) {
         rd_ok = abi_scene_digest(mesh_num, bvh_nodes_device, triangles_device, sphere_num, spheres_device,
                                  sky_cube_map_device, mesh_textures_device, &config, &rd);
+        t_digest = ms() - t_image;
+        if (!(rd_ok && ctx->raw_valid && ctx->raw == rd)) same = false;
+    }
+    if (rc == PT_OK && !same) {  // new pointers (or changed bytes after a gap): translate before rendering
+        if (!gap || !rd_ok)
+            rd_ok = abi_scene_digest(mesh_num, bvh_nodes_device, triangles_device, sphere_num, spheres_device,
+                                     sky_cube_map_device, mesh_textures_device, &config, &rd);
         t_digest = ms() - t_image;
         upload(rd, rd_ok);
     }
@@ -1924,6 +1940,7 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
         (void)hipStreamSynchronize(ctx->stream);
     }
     if (direct) { ctx->image256 = own256; ctx->image = nullptr; ctx->image_cap = 0; ctx->own_image = false; }
+    ctx->abi_last_pass = rc == PT_OK ? pass_counter : 0;
     if (timing)
         std::fprintf(stderr, "[pt] path_tracer_kernel pass %d: image %.3f, scene %.3f%s, launch + digest %.3f (digest %.3f), "
                      "wait + copy + sync %.3f, total %.3f ms\n", pass_counter, t_image, t_scene - t_image,

@@ -43,6 +43,18 @@ def owned_pixels(width: int, height: int, band_rows: int, band_count: int, band_
     return (rows[:, None] * width + np.arange(width)[None, :]).reshape(-1).astype(np.int32)
 
 
+def _placement(rows, most: int, device):
+    """Where the gather's landing rows go on rank 0: row i of rank k's piece (k >= 1) is landing row
+    k * most + i and frame row rows[k][i] (rank 0's own rows are rendered in place). Empty for one rank."""
+    import torch
+
+    if len(rows) == 1:
+        empty = torch.zeros(0, dtype=torch.long, device=device)
+        return empty, empty
+    src = [k * most + torch.arange(len(rows[k]), device=device) for k in range(1, len(rows))]
+    return torch.cat(src), torch.cat([rows[k] for k in range(1, len(rows))])
+
+
 class TiledFrame:
     """One frame of `spp` passes on this rank's bands, collected on rank 0 (world > 1)."""
 
@@ -59,7 +71,10 @@ class TiledFrame:
             raise ValueError(f"unknown frame collective {self.collective!r}")
         self.image = None
         self.stream = None  # the renderer's HIP stream as a torch stream (CUDA buffers only)
-        if self.world > 1:
+        # the collective path runs whenever a process group is given, a one-rank group included (bench.py --rccl:
+        # RCCL's reduce / gather on the one-GPU box, bands = 1)
+        self.collect = self.dist is not None
+        if self.collect:
             import torch
 
             self.image = torch.zeros(width * height * 3, dtype=torch.float32, device=device)
@@ -76,9 +91,7 @@ class TiledFrame:
                 # rank's rows with a single gather + scatter (not one indexing pass per rank)
                 self.landing = torch.zeros(self.world, most, width, 3, dtype=torch.float32, device=device)
                 self.parts = list(self.landing.unbind(0))
-                src = [k * most + torch.arange(len(self.rows[k]), device=device) for k in range(1, self.world)]
-                self.src_rows = torch.cat(src)
-                self.dst_rows = torch.cat([self.rows[k] for k in range(1, self.world)])
+                self.src_rows, self.dst_rows = _placement(self.rows, most, device)
             if self.image.is_cuda and hasattr(renderer, "stream_handle"):
                 self.stream = torch.cuda.ExternalStream(renderer.stream_handle(), device=self.image.device)
         else:
@@ -99,7 +112,7 @@ class TiledFrame:
         all in order on the renderer's HIP stream: no host synchronisation, so several TiledFrames
         (one renderer context each) can have frames in flight and one frame's tail overlaps the next
         frame's start. With a host-side renderer (no stream) every step runs in host order."""
-        if self.world == 1:
+        if not self.collect:
             self.r.render(cam, cfg, 1, spp, write_u8=2)
             return
         with self._on_stream():
@@ -168,7 +181,8 @@ class FrameGroup:
         renderer.setup_frame(width, height, self.images[0].data_ptr())  # the frame geometry
         self.stream = None
         self.last = 0  # frames of the last launch
-        if self.world > 1:
+        self.collect = self.dist is not None  # a one-rank group included (TiledFrame)
+        if self.collect:
             renderer.set_tiling(band_rows, self.world, self.rank)
             self.rows = [torch.as_tensor(owned_rows(height, band_rows, self.world, k), device=device)
                          for k in range(self.world)]
@@ -179,9 +193,7 @@ class FrameGroup:
             if self.rank == 0:
                 self.landing = torch.zeros(self.world, frames, most, width, 3, dtype=torch.float32, device=device)
                 self.parts = list(self.landing.unbind(0))
-                src = [k * most + torch.arange(len(self.rows[k]), device=device) for k in range(1, self.world)]
-                self.src_rows = torch.cat(src)
-                self.dst_rows = torch.cat([self.rows[k] for k in range(1, self.world)])
+                self.src_rows, self.dst_rows = _placement(self.rows, most, device)
         if self.stack.is_cuda and hasattr(renderer, "stream_handle"):
             self.stream = torch.cuda.ExternalStream(renderer.stream_handle(), device=self.stack.device)
 
@@ -201,7 +213,7 @@ class FrameGroup:
         if not 1 <= n <= self.frames:
             raise ValueError(f"1..{self.frames} cameras per launch, got {n}")
         self.last = n
-        if self.world == 1:
+        if not self.collect:
             with self._on_stream():
                 self.r.render_frames(list(cams), cfg, self.images[:n], self.images8[:n], 1, spp, write_u8=2)
             return

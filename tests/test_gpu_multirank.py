@@ -46,6 +46,52 @@ def test_tiled_frames_on_hip_equal_the_oracle(require_gpu, tmp_path, ranks, coll
         assert np.array_equal(img8, ref8), f"context {k}: 8-bit image"
 
 
+def test_rccl_one_rank_metric_frame(require_gpu, tmp_path):
+    """RCCL itself on the one-GPU box: torch.distributed "nccl" with a one-rank group, initialised as bench.py
+    initialises its N-GPU runs (torch.distributed.run env:// rendezvous, device_id), carries the metric frame
+    through the production collective path — a FrameGroup of three frames in one MULTI launch with one RCCL
+    gather, and a TiledFrame with one RCCL reduce — plus an all-reduce and a barrier. Every frame equals the
+    oracle's whole frame bit for bit, and librccl is the library the process loaded."""
+    import bench
+
+    out = str(tmp_path / "rccl")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(HERE, "gpu_rccl_worker.py"), out]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-4000:]
+    import json
+    facts = json.load(open(f"{out}_facts.json"))
+    assert facts["backend"] == "nccl" and facts["world_size"] == 1, facts
+    assert "MULTI" in facts["group_kernel"], facts
+    assert facts["all_reduce"] == [1.5, 2.5] and any("librccl" in p for p in facts["rccl_loaded"]), facts
+    wl = bench.Workload("metric")
+    turned = pt.camera(wl.width, wl.height, yaw=0.35, **wl.cam_kw)
+    ref, ref8, _ = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, wl.spp)
+    ref_t, ref8_t, _ = oracle.render(wl.scene.view, turned, wl.cfg, 1, wl.spp)
+    for tag, (want, want8) in (("group0", (ref, ref8)), ("group1", (ref_t, ref8_t)), ("group2", (ref, ref8)),
+                               ("reduce", (ref, ref8))):
+        img = np.load(f"{out}_{tag}_f.npy")
+        img8 = np.load(f"{out}_{tag}_u8.npy")
+        assert np.array_equal(img.view(np.uint32), want.view(np.uint32)), f"{tag}: float image"
+        assert np.array_equal(img8, want8), f"{tag}: 8-bit image"
+
+
+def test_bench_rccl_one_rank_self_check(require_gpu, tmp_path):
+    """bench.py --rccl at N = 1: the timed run on the distributed path over a one-rank RCCL group (gather, frame
+    groups, barrier, max-over-ranks all-reduce) and its image_matches_1gpu self-check, which re-renders the last
+    timed launch's first and last frame alone; the line must say true, and the run must exit 0."""
+    import json
+    cmd = [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--rccl", "--steps", "10", "--warmup",
+           "2", "--no-cpu-baseline", "--orbit", "0.01"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-4000:]
+    line = json.loads(res.stdout.strip().splitlines()[-1])
+    assert line["config"]["image_matches_1gpu"] is True, line["config"]
+    assert line["config"]["collective"]["backend"] == "nccl", line["config"]
+    assert line["config"]["frames_per_launch"] == 8 and line["config"]["orbit_rad_per_frame"] == 0.01, line["config"]
+
+
 @pytest.mark.parametrize("ranks,collective,inflight,group", [(2, "gather", 3, 4), (3, "reduce", 2, 3)])
 def test_frame_groups_on_hip_equal_the_oracle(require_gpu, tmp_path, ranks, collective, inflight, group):
     """bench.py's PT_BENCH_GROUP path: FrameGroup contexts (pt_render_frames, one collective per group) with

@@ -505,11 +505,17 @@ def test_medium_bound_mode_variants(bench_gpu):
 
 
 def test_c5_4k_textured_depth12_frame(bench_gpu):
-    """BASELINE config C5: three textured knots + a textured cube (diffuse and specular maps) at 3840x2160,
-    depth 12, 8 passes in one launch, whole frame (8.3 M pixels) against the oracle."""
+    """BASELINE config C5 as SURVEY.md §8(d) specifies it: the reference's vanille.obj (twice, 15 shapes each with
+    vanille.json's per-shape materials and its five TGA diffuse maps) with human, cow, monkey and cup, sponza
+    *_spec.tga specular maps (512^2 RGBA, 512^2 RGB, 1024^2 RGB), loaded from c5_vanille_gallery.json by the
+    reference-format scene parser, at 3840x2160, depth 12, 8 passes in one launch: the whole frame (8.3 M
+    pixels) against the oracle."""
     import bench
     wl = bench.Workload("c5")
     assert wl.depth == 12 and (wl.width, wl.height) == (3840, 2160)
+    v = wl.scene.view
+    assert v.texture_num == 8 and v.mesh_num == 8 and v.triangle_num > 100000
+    assert {(v.mesh_textures[i].width, v.mesh_textures[i].height) for i in range(8)} >= {(1024, 1024), (256, 256)}
     launches, _ = _render_workload(bench_gpu, wl, passes=8)
     assert launches == {0: 1, 3: 1}, launches
 
@@ -951,6 +957,72 @@ def test_reference_scene_files(gpu, tmp_path, name, bvh):
     img, img8, ref, ref8, _ = render_both(gpu, sc, cam, cfg, passes=2)
     assert_bitwise(img, ref, f"{name} float")
     assert_bitwise(img8, ref8, f"{name} 8-bit")
+
+
+ASSET_CAMS = {"vanille": dict(center=(0, 0, 0), radius=70.0, pitch=0.1),
+              "vanille_nude": dict(center=(0, 0, 0), radius=70.0, pitch=0.1),
+              "subsurface_scattering_s": dict(center=(0, 0.8, 0), radius=11.0, pitch=0.1),
+              "subsurface_scattering_a": dict(center=(0, 0.8, 0), radius=11.0, pitch=0.1),
+              "dinosaur": dict(center=(0, 0, 0), radius=16.0, pitch=0.15, yaw=1.2)}
+
+
+def _asset_scene(tmp_path, name, depth=8):
+    from test_loader import make_root
+
+    root = make_root(tmp_path, assets=True)
+    cfg = pt.load_config(str(root / "res" / "configuration" / "config.json"))
+    cfg.max_tracer_depth = depth
+    sc = pt.load_scene(str(root / "res" / "scene" / f"{name}.json"), root_dir=str(root), config=cfg,
+                       background="res\\texture\\lobby", background_format="bmp")
+    return sc, cfg
+
+
+@pytest.mark.parametrize("name", list(ASSET_CAMS))
+def test_reference_asset_scene_frames(gpu, tmp_path, name):
+    """The reference's own scenes over its own assets (tests/golden/ref_assets.tar.xz): vanille.json (25,786
+    triangles in 15 shapes with per-shape materials, vanille.json:102, and five TGA diffuse maps of 256^2-1024^2),
+    vanille_nude.json (its missing c595_00.tga generated), subsurface_scattering_s.json (five 24k-triangle cups:
+    Green1 is absorption-only, sigma_s' = 0, so its free flights are -log(u) / 0 = +inf; Green2-5 scatter with
+    sigma_s' 5-20), subsurface_scattering_a.json and dinosaur.json; the lobby BMP skybox where theirs is missing
+    (yokohama) or JPEG (lycksele). Whole 320x180 frames, 2 passes, depth 8, under both schedules: bit-exact."""
+    sc, cfg = _asset_scene(tmp_path, name)
+    cam = pt.camera(320, 180, **ASSET_CAMS[name])
+    img, img8, ref, ref8, st = render_both(gpu, sc, cam, cfg, passes=2)
+    assert_bitwise(img, ref, f"{name} float")
+    assert_bitwise(img8, ref8, f"{name} 8-bit")
+    if name == "subsurface_scattering_s":
+        assert st["inf_flight"] > 1000, st  # segments inside Green1 reached the sigma_s' = 0 branch
+
+
+def test_absorption_only_medium_nan_free_flight(gpu, tmp_path):
+    """The free flight of path_tracer_kernel.cu:463-466 over sigma_s' = 0 when the draw is exactly 1.0f:
+    -__logf(1.0f) / 0 = -0 / 0 = NaN, which is never below min_t, so the segment is attenuated over min_t and
+    shades its hit (the +inf case of any other draw goes the same way). subsurface_scattering_s.json with an
+    absorption-only air (sigma_a > 0, sigma_s' = 0, Green1's kind of medium) makes every segment draw a free
+    flight; the pass is chosen so that one pixel's depth-0 draw rounds to 1.0f (the oracle's restatement of the
+    generator finds it: probability ~3e-8 per draw). Passes 1 and that pass, bit-exact, with the oracle counting
+    the NaN flight."""
+    sc, cfg = _asset_scene(tmp_path, "subsurface_scattering_s", depth=6)
+    cfg.air_absorption_coef = pt._abi.Float3(0.02, 0.03, 0.013)
+    cfg.air_reduced_scattering_coef = pt._abi.Float3(0.0, 0.0, 0.0)
+    W, H = 320, 180
+    cam = pt.camera(W, H, **ASSET_CAMS["subsurface_scattering_s"])
+    pixels = np.arange(W * H)
+    p = next(p for p in range(2, 100000) if (oracle.trace_first_draws(p, pixels, 0) == 1.0).any())
+    hit = np.flatnonzero(oracle.trace_first_draws(p, pixels, 0) == 1.0)
+    gpu.upload(sc, cfg)
+    gpu.setup_frame(W, H)
+    gpu.render(cam, cfg, 1, 1, write_u8=0)
+    gpu.render(cam, cfg, p, 1, write_u8=2)
+    img, img8 = gpu.download()
+    ref = np.zeros((W * H, 3), np.float32)
+    ref8 = np.zeros((W * H, 3), np.uint8)
+    oracle.render(sc.view, cam, cfg, 1, 1, image=ref, image256=ref8)
+    _, _, st = oracle.render(sc.view, cam, cfg, p, 1, image=ref, image256=ref8)
+    assert st["nan_flight"] >= len(hit) >= 1, (p, hit, st)
+    assert st["inf_flight"] > 0, st
+    assert_bitwise(img.reshape(-1, 3), ref, f"pass {p} float")
+    assert_bitwise(img8.reshape(-1, 3), ref8, f"pass {p} 8-bit")
 
 
 def test_device_refit_equals_the_edited_scene(require_gpu):

@@ -40,10 +40,44 @@ def write_bmp24(path, rgb):
         f.write(hdr + info + rows)
 
 
-def make_root(tmp_path, sky=16):
+def write_tga24(path, rgb, top_down=False):
+    """Uncompressed 24-bit true-colour TGA (image type 2, BGR), the format of the reference's vanille maps."""
+    h, w, _ = rgb.shape
+    hdr = bytes([0, 0, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0]) + w.to_bytes(2, "little") + h.to_bytes(2, "little")
+    hdr += bytes([24, 0x20 if top_down else 0])
+    rows = rgb if top_down else rgb[::-1]
+    with open(path, "wb") as f:
+        f.write(hdr + np.ascontiguousarray(rows[..., ::-1]).tobytes())
+
+
+def link_reference_assets(root):
+    """The reference's own meshes, TGA maps and lobby skybox (tests/golden/ref_assets.tar.xz, unpacked once by
+    bench.asset_root) linked into a make_root directory, so vanille.json, vanille_nude.json,
+    subsurface_scattering_{s,a}.json and dinosaur.json load. vanille_nude.json names c595_00.tga, which the
+    reference checkout lacks: a generated 256x256 map stands in for it (and says so in its pixels)."""
+    import bench
+
+    src = os.path.join(bench.asset_root(), "res")
+    for f in os.listdir(os.path.join(src, "obj")):
+        dst = root / "res" / "obj" / f
+        if not dst.exists():
+            os.symlink(os.path.join(src, "obj", f), dst)
+    for d in ("vanille", "sponza", "lobby"):
+        os.symlink(os.path.join(src, "texture", d), root / "res" / "texture" / d)
+    nude = root / "res" / "texture" / "vanille_nude"
+    nude.mkdir()
+    for f in os.listdir(os.path.join(src, "texture", "vanille_nude")):
+        os.symlink(os.path.join(src, "texture", "vanille_nude", f), nude / f)
+    y, x = np.mgrid[0:256, 0:256]
+    write_tga24(str(nude / "c595_00.tga"), np.stack([x, y, (x ^ y) & 0xff], -1).astype(np.uint8))
+    return root
+
+
+def make_root(tmp_path, sky=16, assets=False):
     """A reference-style working directory: res/ from the fixtures plus a generated yokohama skybox
     (absent from the checkout), a generated JPEG maskonaive skybox (micro_surface.json; the
-    reference's 2048^2 faces are too large for fixtures) and the tex_cube texture."""
+    reference's 2048^2 faces are too large for fixtures) and the tex_cube texture; with `assets`, also the
+    reference's own larger meshes and textures (link_reference_assets)."""
     root = tmp_path / "gpt"
     shutil.copytree(RES, root / "res")
     rng = np.random.default_rng(11)
@@ -61,6 +95,8 @@ def make_root(tmp_path, sky=16):
     tex_dir = root / "res" / "texture" / "tex_cube"
     tex_dir.mkdir(parents=True)
     PIL.fromarray(rng.integers(0, 256, (24, 40, 4), dtype=np.uint8), "RGBA").save(str(tex_dir / "uv.png"))
+    if assets:
+        link_reference_assets(root)
     return root
 
 
@@ -306,6 +342,56 @@ def test_reference_scene_files_load(tmp_path, name):
             assert got.mat.medium.refraction_index == np.float32(float(m["RefractionIndex"]))
         else:
             assert bytes(got.mat) == bytes(pt.material_preset(s["Material"]))
+
+
+@pytest.mark.parametrize("name", ["vanille", "vanille_nude", "subsurface_scattering_s", "subsurface_scattering_a",
+                                  "dinosaur", "c5_vanille_gallery"])
+def test_reference_asset_scenes_load(tmp_path, name):
+    """The reference's scenes over its own larger assets (tests/golden/ref_assets.tar.xz), background swapped to the
+    lobby BMP skybox where theirs is missing (yokohama) or JPEG (dinosaur's lycksele). Every mesh triangle carries
+    the material its OBJ shape maps to (Core/triangle_mesh.cpp:185: shape i takes Material[i], the last one past
+    the end), custom materials by value from the file, textures decoded at their own sizes."""
+    root = make_root(tmp_path, assets=True)
+    cfg = pt.load_config(str(root / "res" / "configuration" / "config.json"))
+    sc = pt.load_scene(str(root / "res" / "scene" / f"{name}.json"), root_dir=str(root), config=cfg,
+                       background="res\\texture\\lobby", background_format="bmp")
+    spec = json.load(open(os.path.join(RES, "scene", f"{name}.json")))
+    v = sc.view
+    assert v.mesh_num == len(spec["Mesh"]) and v.texture_num == len(spec.get("Texture", []))
+    assert v.sky_cube_map.contents.length == 512
+    custom = {m["Name"]: m for m in spec.get("Material", [])}
+    t0 = 0
+    for mesh in spec["Mesh"]:
+        path = str(root / mesh["Path"].replace("\\", "/"))
+        shapes = pt.load_obj(path)
+        for i, s in enumerate(shapes):
+            want = mesh["Material"][min(i, len(mesh["Material"]) - 1)]
+            for t in (t0, t0 + len(s.vertices) - 1):
+                got = v.triangles[t].mat.contents
+                if want in custom:
+                    m = custom[want]
+                    assert (got.diffuse_color.x, got.specular_color.x) == (np.float32(m["Diffuse"].split()[0]),
+                                                                          np.float32(m["Specular"].split()[0]))
+                    assert got.medium.scattering.absorption_coefficient.x == np.float32(m["AbsorptionCoef"].split()[0])
+                    assert got.medium.scattering.reduced_scattering_coefficient.x == np.float32(
+                        m["ReducedScatteringCoef"].split()[0])
+                    # no texcoords in the OBJ: the diffuse map is disabled (triangle_mesh.cpp:131-137)
+                    want_tex = int(m.get("DiffuseTextureId", "-1")) if s.uvs is not None else -1
+                    assert got.diffuse_texture_id == want_tex
+                    assert got.specular_texture_id == int(m.get("SpecularTextureId", "-1"))
+                else:
+                    assert bytes(got) == bytes(pt.material_preset(want))
+            t0 += len(s.vertices)
+    assert t0 == v.triangle_num
+    for i, rel in enumerate(spec.get("Texture", [])):
+        tw = v.mesh_textures[i]
+        want = np.asarray(PIL.open(str(root / rel.replace("\\", "/"))).convert("RGB"))
+        assert (tw.height, tw.width) == want.shape[:2]
+        px = np.ctypeslib.as_array(tw.pixels, (tw.height * tw.width * 4,)).reshape(tw.height, tw.width, 4)
+        assert np.array_equal(px[..., :3], want) and (px[..., 3] == 255).all()
+    if name == "subsurface_scattering_s":  # Green1: an absorption-only medium (sigma_s' = 0)
+        g1 = custom["Green1"]
+        assert g1["ReducedScatteringCoef"] == "0.0 0.0 0.0" and g1["AbsorptionCoef"] == "20.0 3.0 13.0"
 
 
 def test_scene_rules_and_errors(tmp_path):

@@ -86,7 +86,7 @@ def _worker(rank, world, port, out_dir, collective="gather", inflight=1):
         if inflight == 1:
             r = OracleFrameRenderer(scene)
             frame = pt.TiledFrame(r, W, H, dist, BAND, device="cpu", collective=collective)
-            assert frame.world == world and frame.rank == rank
+            assert frame.world == world and frame.rank == rank and frame.collect
             for _ in range(2):  # a second frame must not see the first one's reduced sum (bench renders many)
                 frame.render(cam, cfg, SPP)
         else:
@@ -136,8 +136,11 @@ def _group_worker(rank, world, port, out_dir, collective):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,collective", [(2, "gather"), (3, "gather"), (2, "reduce")])
+@pytest.mark.parametrize("world,collective", [(2, "gather"), (3, "gather"), (2, "reduce"), (1, "gather"),
+                                              (1, "reduce")])
 def test_frame_group_equals_single_renders(tmp_path, world, collective):
+    """World size 1 is bench.py --rccl's path: a one-rank group still takes the collective (band count 1, the
+    gather's own piece placed, or the reduce of the one buffer)."""
     mp.start_processes(_group_worker, args=(world, _free_port(), str(tmp_path), collective), nprocs=world,
                        join=True, start_method="spawn")
     r0 = np.load(tmp_path / "rank0.npz")
@@ -196,7 +199,8 @@ def test_deal_bands_gives_every_region_its_costliest_bands_first(n, partial):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world,collective,inflight", [(2, "gather", 1), (2, "reduce", 1), (3, "gather", 1),
-                                                       (2, "gather", 2), (2, "reduce", 3)])
+                                                       (2, "gather", 2), (2, "reduce", 3), (1, "gather", 1),
+                                                       (1, "reduce", 2)])
 def test_two_rank_tiled_frame_equals_single_render(tmp_path, world, collective, inflight):
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), collective, inflight), nprocs=world, join=True,
                        start_method="spawn")
