@@ -267,6 +267,12 @@ def main() -> int:
                          "bands = 1, the frame's gather / reduce, barrier and all-reduce on RCCL, and the "
                          "image_matches_1gpu self-check")
     args = ap.parse_args()
+    # stdout carries exactly ONE line, the JSON result: everything else the process prints — the scene loader's
+    # progress, RCCL's version banner at communicator init (printed to stdout by the library itself) — goes to
+    # stderr, at the file-descriptor level so that native code's writes follow it
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     heavy = args.workload in ("c4", "c5")
     if args.steps is None:
         args.steps = 3 if heavy else 20
@@ -627,7 +633,7 @@ def main() -> int:
         line["cpu_baseline"] = cpu_baseline(wl, threads)
         line["cpu_baseline"]["cpu"] = platform.processor() or platform.machine()
         line["cpu_baseline"]["threads_from"] = why
-    print(json.dumps(line), flush=True)
+    print(json.dumps(line), file=result_out, flush=True)
     if distributed:
         dist.destroy_process_group()
         if not matches_1gpu:

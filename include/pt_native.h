@@ -46,11 +46,13 @@ int pt_scene_info(pt_context* ctx, long long* device_bytes, int* node_num, int* 
  * with several contexts rendering frames in flight, the rest of the CUs run the other frames
  * (DESIGN.md §6). Results do not depend on it. */
 int pt_set_grid_share(pt_context* ctx, int percent);
-/* Tolerance mode (default off; -1 = the PT_MEDIUM_BOUND environment variable, "1" = on): the persistent kernel
- * walks an in-medium segment's meshes with min_t starting at the segment's free-flight distance (1 + 2^-10),
- * which it draws first, instead of infinity. Not proven bit-exact against the reference walk
- * (a ray grazing a triangle's plane can make Moller-Trumbore's t fall below its box's entry); measured
- * bit-identical on the whole C4 frame. Other schedules ignore it. */
+/* Tolerance mode (default off; -1 = the PT_MEDIUM_BOUND environment variable, "1" = on, for contexts this API
+ * creates; the reference ABI's own context ignores the environment and is on only through this call): the
+ * persistent kernel pass_kernel_u and the instrumented pass_kernel (trace_step) walk an in-medium segment's
+ * meshes with min_t starting at the segment's free-flight distance (1 + 2^-10), which they draw first, instead
+ * of infinity. The wavefront schedule ignores it. Not proven bit-exact against the reference
+ * walk (a ray grazing a triangle's plane can make Moller-Trumbore's t fall below its box's entry); measured
+ * bit-identical on the whole C4 frame and on subsurface_scattering_s/_a. */
 int pt_set_medium_bound(pt_context* ctx, int on);
 /* Band order of the work queue. The context's pixels are bands of band_rows rows
  * (pt_set_tiling; one context: bands of the whole frame). pt_band_count gives their number and whether

@@ -32,6 +32,12 @@ namespace pt {
 #ifndef PT_PROF_MESH
 #define PT_PROF_MESH 0
 #endif
+// PT_GEN_RING (default 1): pass_kernel_u generates camera paths a whole chunk at a time, by the full wave, into a
+// per-wave LDS ring that refills pop from (gen_ring_fill / gen_ring_take). 0: each refill generates its own
+// lanes' paths (round 4's refill: 9.2 lanes per generation instruction on the metric frame).
+#ifndef PT_GEN_RING
+#define PT_GEN_RING 1
+#endif
 template <class T>
 __device__ __forceinline__ void opaque(T& x) {
     int* p = reinterpret_cast<int*>(&x);
@@ -315,6 +321,30 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
     }
 }
 
+// ---- the generation ring (PT_GEN_RING) ---------------------------------------------------------------------
+// generate_ray_kernel (:299-379) runs once per new path. Generated where a refill hands out units, it executes
+// with only the refilled lanes active: 9.2 of 64 on the metric frame, 7 % of the kernel's VALU (round 4's PT_DUP
+// split). Here a wave that runs out of generated paths fetches its next chunk of units (one returning atomic, as
+// before) and ALL its lanes generate the chunk's camera paths at once, lane i unit i, into the wave's 64-entry
+// ring in LDS; refills then pop entries in lane order. An entry is 32 B: {origin, path seed} {direction, unit}.
+// The other per-path fields are constants at generation (throughput 1, radiance 0, air, depth 0). Every path is
+// still the generate_path of its (pass, pixel): only which instruction serves it changes.
+#define PT_RING 64
+__device__ __forceinline__ void gen_ring_put(float4* ring, int e, const PathState& ps, int32_t pseed, unsigned int unit) {
+    ring[2 * e] = make_float4(ps.o.x, ps.o.y, ps.o.z, __int_as_float(pseed));
+    ring[2 * e + 1] = make_float4(ps.d.x, ps.d.y, ps.d.z, __uint_as_float(unit));
+}
+__device__ __forceinline__ void gen_ring_get(const float4* ring, int e, PathState& ps, int32_t& pseed, unsigned int& unit) {
+    const float4 a = ring[2 * e], b = ring[2 * e + 1];
+    ps.o = mk3(a.x, a.y, a.z);
+    ps.d = mk3(b.x, b.y, b.z);
+    ps.thr = mk3(1.0f, 1.0f, 1.0f);
+    ps.rad = mk3(0.0f, 0.0f, 0.0f);
+    ps.medium = -1;
+    pseed = __float_as_int(a.w);
+    unit = __float_as_uint(b.w);
+}
+
 // PROF: wave-level occupancy counters of the state machine into stats[16..31] (tools/uprof.py):
 // rounds, walk steps, walking lanes summed over steps, shading batches, lanes shaded, triangle
 // batches, lanes in triangle batches, lanes refilled, then cycles and the drained/ready/idle counts,
@@ -333,6 +363,11 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     __shared__ int2 lds_mesh[PT_LDS_MESHES];
     __shared__ int4 lds_next[PT_LDS_MESHES + 1];
     __shared__ float4 lds_root[2 * PT_ROOT_MESHES];
+#if PT_GEN_RING
+    __shared__ float4 lds_ring[PT_UBLOCK / 64][2 * PT_RING];  // one generation ring per wave
+    float4* ring = lds_ring[threadIdx.x >> 6];
+    int ring_head = 0, ring_end = 0;  // wave-uniform: entries [ring_head, ring_end) are generated, not yet taken
+#endif
     extern __shared__ float4 lds_dyn[];
     DevMaterial* lds_mats = reinterpret_cast<DevMaterial*>(lds_dyn);
     {
@@ -412,6 +447,83 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         // lanes without a path take the next (pixel, pass) units, one atomic per wave (pt_work.h)
         const bool want = mode == LANE_WANT;
         const unsigned long long need_mask = __ballot(want);
+#if PT_GEN_RING
+        if (need_mask) {
+            // lanes take generated paths from the ring in lane order; when it runs dry the wave fetches the next
+            // chunk and generates all of it (gen_ring_fill below), then the remaining lanes take from the new ring
+            const int taken = __popcll(need_mask);
+            const int rank = __popcll(need_mask & lanes_below(lane));
+            const int avail = ring_end - ring_head;
+            bool got = false;
+            unsigned int u = ~0u;
+            if (want && rank < avail) {
+                gen_ring_get(ring, ring_head + rank, ps, pseed, u);
+                got = true;
+            }
+            if (taken <= avail) {
+                ring_head += taken;
+            } else if (!drained && work_fetch(out.fetch, regions.stride, regions, (unsigned int)chunk, cursor)) {
+                const int n = (int)(cursor.end - cursor.cur);  // <= chunk <= PT_RING (host-checked)
+                if (PROF) { prof[7] += (unsigned long long)n; gen_batches++; }
+                // gen_ring_fill: lane i generates unit cursor.cur + i. The camera is read through the scalar cache,
+                // so a chunk that spans frames (MULTI) is generated one frame at a time
+                if (lane < n) {
+                    const unsigned int gu = cursor.cur + (unsigned int)lane;
+                    unsigned int lu = gu;
+                    int frame = 0;
+                    if (MULTI) {
+                        while (lu >= frame_units) { lu -= frame_units; frame++; }
+                    }
+                    bool pending = true;
+                    while (pending) {  // once, unless the chunk spans frames
+                        const int f0 = MULTI ? __builtin_amdgcn_readfirstlane(frame) : 0;
+                        if (frame == f0) {
+                            const int pixel = unit_to_pixel(til, lu >> batch_log2);
+                            const int32_t hseed = hash_pt(first_pass + (int)(lu & ((1u << batch_log2) - 1u)));
+                            const DevCamera cam = MULTI ? load_const(out.cams + f0) : load_const(&P->cam);
+                            PathState g;
+                            if (PT_DUP == 4) {
+                                PathState p2; int px2 = pixel, hs2 = hseed;
+                                opaque(px2); opaque(hs2);
+                                generate_path(cam, cfg, px2, hs2, &p2);
+                                opaque(p2);
+                            }
+                            generate_path(cam, cfg, pixel, hseed, &g);
+                            gen_ring_put(ring, lane, g, path_seed(hseed, pixel), gu);
+                            pending = false;
+                        }
+                    }
+                }
+                cursor.cur = cursor.end;
+                __builtin_amdgcn_wave_barrier();  // the ring's writes before the lanes read it (one wave: in order)
+                const int rest = taken - avail;
+                if (want && !got && rank - avail < n) {
+                    gen_ring_get(ring, rank - avail, ps, pseed, u);
+                    got = true;
+                }
+                ring_head = rest < n ? rest : n;
+                ring_end = n;
+            } else {
+                ring_head = ring_end;
+                drained = true;
+            }
+            if (PROF && drained && t_drain == 0) t_drain = __builtin_amdgcn_s_memrealtime();
+            if (want) {
+                if (got) {
+                    unit = u;
+                    depth = 0;
+                    if (cfg.max_depth > 0) {
+                        mode = LANE_NEW;
+                    } else {
+                        finish_unit(til, cfg, out, ps, unit, MULTI ? frame_local(unit, frame_units) : unit, first_pass,
+                                    write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
+                    }
+                } else if (drained) {
+                    mode = LANE_DONE;
+                }
+            }
+        }
+#else
         if (need_mask) {
             const unsigned int u = work_take(out.fetch, regions.stride, regions, (unsigned int)chunk, need_mask, want,
                                              lanes_below(lane), cursor, drained);
@@ -450,6 +562,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 }
             }
         }
+#if !PT_GEN_RING
         // MULTI: lanes holding a new unit start its camera path. The camera is read through the scalar cache, so
         // one refill starts the paths of one frame: those of the first such lane's frame; a lane whose unit lies
         // in another frame (a refill that spans two frames' units) starts in the next round
@@ -476,6 +589,8 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 }
             }
         }
+#endif
+#endif
         if (mode == LANE_NEW) {
             if (FEAT & PT_FEAT_MBOUND) {
                 wbound = medium_bound(sc, cfg, ps.medium, depth, pseed);
@@ -909,8 +1024,9 @@ using PassFnU = void (*)(const LaunchParams*, int, int, int, int, int, int, int,
 // pass_kernel_u specialised on the scene's features (pt_path.h PT_FEAT_*): feat is what the scene can reach;
 // PT_FEAT_SPECIALISE=0 keeps the all-features kernel. `feat_used` receives the instance's features, so the
 // kernel description names the kernel that runs. PT_UPROF=1: the profiling instance (6 waves, all features).
-// multi: the MULTI instance of the feature set's default wave count (pt_render_frames; PT_MIN_WAVES and
-// PT_UPROF do not apply to it).
+// multi: the MULTI instance (pt_render_frames) for pass_min_waves' choice: 8 or 7 waves without textures or
+// media, 7 with textures, 6 with a medium (the instances built; PT_UPROF does not apply to it). pass_grid_size
+// sizes the grid from the same instance.
 static PassFnU pass_fn_u(int minw, int feat, bool multi, int* feat_used, int* minw_used) {
     static const int spec = env_int("PT_FEAT_SPECIALISE", 1, 0, 1);
     static const int prof = env_int("PT_UPROF", 0, 0, 1);
@@ -919,7 +1035,7 @@ static PassFnU pass_fn_u(int minw, int feat, bool multi, int* feat_used, int* mi
         feat &= PT_FEAT_ALL;
         *feat_used = feat;
         *minw_used = (feat & PT_FEAT_MEDIUM) ? 6 : 7;
-        if (feat == 0 && minw == 8) { *minw_used = 8; return pass_kernel_u<8, false, 0, true>; }
+        if (feat == 0 && minw >= 8) { *minw_used = 8; return pass_kernel_u<8, false, 0, true>; }
         switch (feat) {
             case 0: return pass_kernel_u<7, false, 0, true>;
             case 1: return pass_kernel_u<6, false, 1, true>;
@@ -1007,7 +1123,8 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
         // measured best with frames in flight (7 steps since the end of round 3: metric
         // +0.4 %, C3 +0.9 %, C4/C5 +0.1-0.3 %, profiles/r03/walk_steps/; 4 parked lanes instead of 6 since the
         // fused multiply-adds made the triangle test cheaper: +0.3 % over four rounds, profiles/r04/knobs/)
-        static const int chunk = env_int("PT_CHUNK_MEGA", 64, 0, 4096);
+        // (the generation ring holds one chunk: 1..64 units)
+        static const int chunk = PT_GEN_RING ? env_int("PT_CHUNK_MEGA", 64, 1, PT_RING) : env_int("PT_CHUNK_MEGA", 64, 0, 4096);
         // the shading batch waits for 40 ready lanes with a medium walked exactly (the medium step makes a batch
         // dearer: C4 5952-5966 vs 5747 Mrays/s, 36: 5936-5952, 44: 5814, profiles/r04/knobs/c4_c5_shade_min.txt),
         // 28 otherwise (C5 at 32 / 36: ±0 / -1 %; the medium-bounded walk, shorter: 9450 at 40 vs 9573-9597)

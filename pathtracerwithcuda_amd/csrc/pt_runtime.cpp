@@ -493,7 +493,7 @@ struct pt_context {
     unsigned int* band_cost = nullptr;
     int band_cost_n = 0;
     bool band_cost_on = false;
-    int grid[2][2][8][2] = {};
+    int grid[2][2][8][2][2] = {};  // [leaf1][stats][feat][small][multi]
     std::vector<hipEvent_t> ev_start, ev_stop;
     std::vector<int> ev_kind;          // 0 pass (single-kernel schedule), 1 extend, 2 shade, 3 finalize
     size_t ev_used = 0;
@@ -844,11 +844,13 @@ PassChoice pass_choice(const pt_context* ctx, int feat) {
     return pc;
 }
 
-// small: a launch of fewer than PT_SMALL_LAUNCH units (its kernel may run fewer waves, pass_min_waves)
-int pass_grid(pt_context* ctx, int feat, bool small = false) {
+// small: a launch of fewer than PT_SMALL_LAUNCH units (its kernel may run fewer waves, pass_min_waves); multi: the
+// pt_render_frames instance (its own occupancy: the grid is sized from the instance that runs)
+int pass_grid(pt_context* ctx, int feat, bool small = false, bool multi = false) {
     PassChoice pc = pass_choice(ctx, feat);
     pc.small = small;
-    int& g = ctx->grid[pc.leaf1 ? 1 : 0][pc.stats ? 1 : 0][feat & 7][small ? 1 : 0];
+    pc.multi = multi;
+    int& g = ctx->grid[pc.leaf1 ? 1 : 0][pc.stats ? 1 : 0][feat & 7][small ? 1 : 0][multi ? 1 : 0];
     if (g == 0) {
         g = pass_grid_size(pc, pass_lds_bytes(ctx));
         // PT_GRID_PCT: experiment knob, a percentage of the occupancy-sized grid
@@ -1169,7 +1171,7 @@ int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, con
         if (rc != PT_OK) return rc;
         pc.small = (((long long)units * frames) << lg) < PT_SMALL_LAUNCH;
         ctx->last_kernel = pass_kernel_desc(pc, pass_lds_bytes(ctx));
-        const int g = shared_grid(ctx, pass_grid(ctx, feat, pc.small));
+        const int g = shared_grid(ctx, pass_grid(ctx, feat, pc.small, pc.multi));
         PT_HIP(launch_pass(ctx->params, pc, first, lg, w8, g, pass_lds_bytes(ctx), ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;
@@ -1321,6 +1323,10 @@ pt_context* default_context() {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) dev = 0;
         if (pt_context_create(dev, &g_default) != PT_OK) g_default = nullptr;
+        // the reference ABI's context is bit-exact whatever the environment says: the medium-bounded walk (a
+        // tolerance mode) is off there unless pt_set_medium_bound turns it on explicitly; PT_MEDIUM_BOUND only
+        // sets the default of contexts the native API creates
+        if (g_default) g_default->medium_bound = 0;
     }
     return g_default;
 }

@@ -108,8 +108,9 @@ struct DevConfig {
     float energy_len2;  // energy_exist_threshold (the kill test, path_tracer_kernel.cu:612-616)
     float sss_len2;     // sss_threshold (:460)
     float refr_len2;    // 0.000005f (fresnel.h:37, length(refraction) <= 0.000005f)
-    // pt_set_medium_bound (tolerance mode, off by default): pass_kernel_u walks an in-medium segment's meshes
-    // with min_t starting at its free-flight distance (1 + 2^-10) instead of infinity (pt_path.h medium_bound)
+    // pt_set_medium_bound (tolerance mode, off by default): pass_kernel_u (its PT_FEAT_MBOUND instances) and the
+    // instrumented pass_kernel (trace_step) walk an in-medium segment's meshes with min_t starting at its
+    // free-flight distance (1 + 2^-10) instead of infinity (pt_path.h medium_bound); the wavefront kernels ignore it
     int medium_bound;
 };
 
