@@ -367,6 +367,10 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     __shared__ float4 lds_ring[PT_UBLOCK / 64][2 * PT_RING];  // one generation ring per wave
     float4* ring = lds_ring[threadIdx.x >> 6];
     int ring_head = 0, ring_end = 0;  // wave-uniform: entries [ring_head, ring_end) are generated, not yet taken
+    // the lane's (pixel, pass) unit lives in LDS: it is read once, at the path's end (finish_unit), and held in a
+    // VGPR it was spilled to scratch around the ring fill (written back after every shading batch: 0.6 GB of
+    // scratch writes per launch)
+    __shared__ unsigned int lds_unit[PT_UBLOCK];
 #endif
     extern __shared__ float4 lds_dyn[];
     DevMaterial* lds_mats = reinterpret_cast<DevMaterial*>(lds_dyn);
@@ -469,18 +473,19 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 // so a chunk that spans frames (MULTI) is generated one frame at a time
                 if (lane < n) {
                     const unsigned int gu = cursor.cur + (unsigned int)lane;
-                    unsigned int lu = gu;
-                    int frame = 0;
-                    if (MULTI) {
-                        while (lu >= frame_units) { lu -= frame_units; frame++; }
-                    }
-                    bool pending = true;
-                    while (pending) {  // once, unless the chunk spans frames
-                        const int f0 = MULTI ? __builtin_amdgcn_readfirstlane(frame) : 0;
-                        if (frame == f0) {
+                    // the chunk's frames f_lo..f_hi are wave-uniform (scalar arithmetic on the chunk's bounds): one
+                    // pass per frame, each lane generating in its own frame's pass (one pass unless the chunk spans
+                    // frames)
+                    const unsigned int c0 = (unsigned int)__builtin_amdgcn_readfirstlane((int)cursor.cur);
+                    const unsigned int f_lo = MULTI ? c0 / frame_units : 0u;
+                    const unsigned int f_hi = MULTI ? (c0 + (unsigned int)n - 1u) / frame_units : 0u;
+                    for (unsigned int f = f_lo; f <= f_hi; f++) {
+                        const unsigned int base = f * frame_units;
+                        if (!MULTI || (gu >= base && gu - base < frame_units)) {
+                            const unsigned int lu = gu - base;
                             const int pixel = unit_to_pixel(til, lu >> batch_log2);
                             const int32_t hseed = hash_pt(first_pass + (int)(lu & ((1u << batch_log2) - 1u)));
-                            const DevCamera cam = MULTI ? load_const(out.cams + f0) : load_const(&P->cam);
+                            const DevCamera cam = MULTI ? load_const(out.cams + f) : load_const(&P->cam);
                             PathState g;
                             if (PT_DUP == 4) {
                                 PathState p2; int px2 = pixel, hs2 = hseed;
@@ -490,7 +495,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                             }
                             generate_path(cam, cfg, pixel, hseed, &g);
                             gen_ring_put(ring, lane, g, path_seed(hseed, pixel), gu);
-                            pending = false;
                         }
                     }
                 }
@@ -510,12 +514,12 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (PROF && drained && t_drain == 0) t_drain = __builtin_amdgcn_s_memrealtime();
             if (want) {
                 if (got) {
-                    unit = u;
+                    lds_unit[threadIdx.x] = u;
                     depth = 0;
                     if (cfg.max_depth > 0) {
                         mode = LANE_NEW;
                     } else {
-                        finish_unit(til, cfg, out, ps, unit, MULTI ? frame_local(unit, frame_units) : unit, first_pass,
+                        finish_unit(til, cfg, out, ps, u, MULTI ? frame_local(u, frame_units) : u, first_pass,
                                     write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
                     }
                 } else if (drained) {
@@ -623,7 +627,12 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (mode == LANE_READY) {  // the pass's end for this unit, or the next trace step
                 depth++;
                 if (!alive || depth >= cfg.max_depth) {
-                    finish_unit(til, cfg, out, ps, unit, MULTI ? frame_local(unit, frame_units) : unit, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
+#if PT_GEN_RING
+                    const unsigned int un = lds_unit[threadIdx.x];
+#else
+                    const unsigned int un = unit;
+#endif
+                    finish_unit(til, cfg, out, ps, un, MULTI ? frame_local(un, frame_units) : un, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
                     mode = LANE_WANT;
                 } else {
                     mode = LANE_NEW;  // its next segment starts in the next round's refill, with the new paths

@@ -504,6 +504,43 @@ def test_medium_bound_mode_variants(bench_gpu):
         assert got == {"segments": st["segments"], "nodes": st["nodes"], "tris": st["tris"]}
 
 
+@pytest.mark.parametrize("name", ["subsurface_scattering_s", "subsurface_scattering_a", "air_sigma_s_0.5"])
+def test_medium_bound_mode_reference_media(bench_gpu, tmp_path, name):
+    """The medium-bounded walk beyond DragonGreen (sigma_s' = 400, mean free path 0.0025): the reference's five
+    subsurface cups of subsurface_scattering_s.json (Green1 absorption-only, Green2-5 sigma_s' 5-20: mean free
+    paths 0.05-0.2, longer flights that prune less and graze more) and subsurface_scattering_a.json (Absorp1-5,
+    sigma_s' 5, sigma_a 0-10), and a scattering air over the metric scene (sigma_s' 0.5: every segment in a
+    medium). Whole 960x540 frames, 4 passes: the HIP frame equals the oracle's bounded walk bit for bit, and the
+    bounded walk stays within the stated tolerance of the reference's exact walk (measured
+    identical, every pixel and every path, on the whole 1920x1080 frames: profiles/r05/medium_bound/)."""
+    if name.startswith("air"):
+        sc = pt.cornell_scene(pt.torus_knot(350, 100))
+        cfg = pt.configuration(max_tracer_depth=8, air_absorption_coef=(0.02, 0.03, 0.05),
+                               air_reduced_scattering_coef=(0.5, 0.5, 0.5))
+        cam = pt.camera(960, 540, **BENCH_CAM)
+    else:
+        sc, cfg = _asset_scene(tmp_path, name)
+        cam = pt.camera(960, 540, **ASSET_CAMS[name])
+    r = bench_gpu
+    r.set_medium_bound(True)
+    try:
+        r.upload(sc, cfg)
+        r.setup_frame(960, 540)
+        r.render(cam, cfg, 1, 4, write_u8=2)
+        img, img8 = r.download()
+        assert "FEAT=5" in r.last_kernel() or "FEAT=7" in r.last_kernel(), r.last_kernel()
+    finally:
+        r.set_medium_bound(None)
+    ref, ref8, sb = oracle.render(sc.view, cam, cfg, 1, 4, medium_bound=True, signatures=True)
+    assert_bitwise(img.reshape(-1, 3), ref, f"bounded {name} float")
+    assert_bitwise(img8.reshape(-1, 3), ref8, f"bounded {name} 8-bit")
+    exact, _, se = oracle.render(sc.view, cam, cfg, 1, 4, signatures=True)
+    assert sb["nodes"] < 0.9 * se["nodes"], (sb["nodes"], se["nodes"])  # the walk really is bounded
+    d = np.abs(ref.astype(np.float64) - exact).max(axis=1)
+    flipped = (se["signatures"] != sb["signatures"]).any(axis=0)
+    assert (d <= 1e-3).mean() >= 0.998 and flipped.mean() <= 0.03 and ((d > 1e-3) & ~flipped).mean() <= 0.001
+
+
 def test_c5_4k_textured_depth12_frame(bench_gpu):
     """BASELINE config C5 as SURVEY.md §8(d) specifies it: the reference's vanille.obj (twice, 15 shapes each with
     vanille.json's per-shape materials and its five TGA diffuse maps) with human, cow, monkey and cup, sponza
@@ -690,22 +727,30 @@ def test_edge_cases(gpu, case):
     assert_bitwise(img8.reshape(-1, 3), ref8, f"{case} 8-bit")
 
 
-@pytest.mark.parametrize("case", ["one_launch", "odd_range", "tiled", "grid_share"])
+@pytest.mark.parametrize("case", ["one_launch", "odd_range", "tiled", "grid_share", "depth0", "tiny_frames"])
 def test_render_frames_equal_separate_frames(gpu, case):
     """pt_render_frames: several frames, each through its own camera, in one pass launch per batch of passes
     (the persistent schedule; the wavefront schedule renders them one after another). Every frame is the
     oracle's frame of its camera bit for bit, 8-bit output included, and frame f's radiances are summed into
-    its own image. Cases: one 8-pass launch; a continuation range 2..4 (batches of 2 and 1, the
-    one-pass launch through pass_rad too); a 3-band share (rows of band 1 only); a 45 % grid. The frames' units
-    are laid out in 64-unit blocks (pt_scene.h multi_frame_stride) and a refill takes one block's units, so all
-    of its new paths share a frame and a camera."""
+    its own image. Cases: one 8-pass launch; a continuation range 2..4 (batches of 2 and 1, the one-pass launch
+    through pass_rad too); a 3-band share (rows of band 1 only); a 45 % grid; max_depth 0 (every path ends at
+    generation, through the MULTI instance's finish); 4x2 frames (8 pixels x 8 passes = 64 units: one chunk can
+    hold units of several frames).
+
+    The frames' units follow each other (frame f's unit u is f * units_per_frame + u). A wave's chunk of 64 units
+    (pt_work.h) is generated whole into the wave's LDS ring (pass_kernel_u gen_ring_fill); the camera is read
+    through the scalar cache, so a chunk that holds units of two or more frames is generated frame by frame (the
+    lanes of the first pending lane's frame, then the next). With W x H = 70 x 45 and 8 passes a frame is 25,200
+    units, not a multiple of 64, so some chunk straddles every frame boundary (asserted below)."""
     import torch
 
     sc = pt.cornell_scene(pt.torus_knot(60, 16), cube_length=32)
-    cfg = pt.configuration(max_tracer_depth=6)
-    W, H = 70, 45  # 3150 pixels: a frame's units are not a whole number of 64-unit blocks (padding skipped)
+    cfg = pt.configuration(max_tracer_depth=0 if case == "depth0" else 6)
+    W, H = (4, 2) if case == "tiny_frames" else (70, 45)
     cams = [pt.camera(W, H, yaw=y, **BENCH_CAM) for y in (0.0, 0.4, -0.7)]
     first, count = (2, 3) if case == "odd_range" else (1, 8)
+    if case in ("one_launch", "depth0"):
+        assert (W * H * count) % 64 != 0  # a chunk spans the boundary between frames 0 and 1
     gpu.upload(sc, cfg)
     gpu.setup_frame(W, H)
     if case == "tiled":

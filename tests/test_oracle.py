@@ -154,6 +154,13 @@ def _assert_within_stated_tolerance(subset, model):
     assert ((d > 1e-3) & clean).sum() <= 0.001 * len(sel)
     rel = (np.abs(diff) / np.maximum(np.abs(a), 1e-3)).max(axis=1)[clean]
     assert np.percentile(rel, 99) <= 1e-4 and np.percentile(rel, 99.9) <= 2e-3
+    # no bias over the unflipped pixels: their mean shift stays <= 1e-5 x their mean (<= 1e-4 under the CUDA
+    # intrinsic model, whose error directions are keyed by input and so do not cancel). Measured on these samples:
+    # libm 8.2e-7, plain -1.9e-6, plain+libm -3.1e-6, fma 5e-10, cuda 4.6e-5, cuda_site -8.5e-7; C4: <= 6e-7. A
+    # contraction site placed where the CUDA build has none (or the reverse) moves every pixel it touches the
+    # same way, which this catches where per-pixel bounds do not
+    shift = abs(diff[clean].mean()) / a[clean].mean()
+    assert shift <= (1e-4 if model in ("cuda", "plain+cuda") else 1e-5), shift
     if model == "fma":
         # gcc's own contraction (-ffp-contract=fast) of the whole oracle finds the explicit fmaf sites and
         # only adds ones inside the Cephes stand-ins: >= 99 % of pixels the same bits (whole metric frame:

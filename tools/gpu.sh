@@ -9,6 +9,11 @@
 #   gpurun -- bash tools/gpu.sh profile <tag>                     # rocprof traces + PMC passes + PT_UPROF + PT_DUP
 #   gpurun -- bash tools/gpu.sh orbit <tag>                       # static vs per-frame camera, with and without groups
 #   gpurun -- bash tools/gpu.sh rccl <tag>                        # bench --rccl + its rocprofv3 RCCL API trace
+#   gpurun -- bash tools/gpu.sh rehearsal <tag>                   # N = 2..8 gloo ranks on the one GPU (bench.py's
+#                                                                  # N > 1 path; tools/gpu_multirank_rehearsal.sh)
+#   gpurun -- bash tools/gpu.sh shares <tag>                      # rank 0's share of N = 2, 4, 8 under PMC
+#                                                                  # (tools/gpu_share_pmc.sh) for the N > 1 roofline
+#   gpurun -- bash tools/gpu.sh tile <tag> [tile_scaling.py args] # per-rank share timing on one GPU
 # Summaries for profiles/: python tools/traffic_summary.py / tools/pmc_summary.py / tools/lane_weighted.py.
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
@@ -76,7 +81,6 @@ profile)
   unset PT_BENCH_INFLIGHT PT_BENCH_GROUP
   timeout -k 10 120 python3 tools/uprof.py metric > $T/uprof_metric.json 2> $T/uprof_metric.err || exit $?
   if [ -d $PKG/lib_dup1 ]; then bash tools/gpu_dup.sh $TAG/dup > $T/dup.log 2>&1 || exit $?; tail -4 $T/dup.log; fi
-  [ -z "$SHARES" ] || bash tools/gpu_share_pmc.sh > $T/share_pmc.log 2>&1 || exit $?
   echo profile done ;;
 orbit)
   for r in 1 2; do
@@ -90,6 +94,12 @@ rccl)
   timeout -k 10 300 python3 bench.py --no-cpu-baseline --rccl > $T/rccl.json 2> $T/rccl.err || exit $?
   line $T/rccl.json rccl
   timeout -k 10 300 rocprofv3 --rccl-trace --kernel-trace --stats --output-format csv -d $T/rccl_trace -o run -- python3 bench.py --no-cpu-baseline --rccl --steps 10 --warmup 2 > $T/rccl_trace.log 2>&1 || exit $? ;;
+rehearsal)
+  bash tools/gpu_multirank_rehearsal.sh $TAG ;;
+shares)
+  bash tools/gpu_share_pmc.sh > $T/share_pmc.log 2>&1 || exit $?; tail -20 $T/share_pmc.log ;;
+tile)
+  timeout -k 10 900 python3 tools/tile_scaling.py "$@" > $T/tile.json 2> $T/tile.err || exit $?; cat $T/tile.json ;;
 *)
   echo "unknown step $STEP"; exit 2 ;;
 esac

@@ -56,5 +56,33 @@ if args.workload:
                                   else None),
         "round": args.round or os.path.basename(os.path.normpath(args.out)),
     }
+    rec = d[args.workload]
+    # the timed mode's kernel (frame groups: the MULTI instance), from the pmc_sq_group8 pass of tools/gpu.sh
+    # profile (tools/share_render.py --group 8: one launch of 8 frames), VALU per frame
+    multi = {}
+    for f in glob.glob(os.path.join(args.src, "pmc_sq_group8", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == "SQ_INSTS_VALU" and "pass_kernel_u<" in r["Kernel_Name"] and ", true>" in r["Kernel_Name"]:
+                multi.setdefault(r["Kernel_Name"].split("(")[0], []).append(float(r["Counter_Value"]))
+    if multi:
+        mk, mv = next(iter(multi.items()))
+        rec["valu_insts_per_frame_timed"] = round(sum(mv) / len(mv) / 8)
+        rec["valu_insts_per_frame_timed_source"] = (f"{os.path.relpath(args.out)}/pmc_sq_group8.json: SQ_INSTS_VALU of "
+                                                    f"{mk} (the MULTI instance the timed launches run) over one "
+                                                    "8-frame launch / 8")
+        json.dump({mk: {"SQ_INSTS_VALU_per_launch": sum(mv) / len(mv), "frames_per_launch": 8}},
+                  open(os.path.join(args.out, "pmc_sq_group8.json"), "w"), indent=1)
+    # the solo launch's average duration in rocprofv3's kernel trace (one frame in flight)
+    for f in glob.glob(os.path.join(args.src, "trace", "**", "*kernel_stats.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if args.kernel in r["Name"]:
+                rec["rocprof_avg_launch_ms"] = round(float(r["AverageNs"]) / 1e6, 4)
+                rec["rocprof_avg_launch_source"] = (f"{os.path.relpath(args.out)}/kernel_stats_one_in_flight.csv "
+                                                    f"({r['Calls']} solo launches)")
+                import shutil
+                shutil.copy(f, os.path.join(args.out, "kernel_stats_one_in_flight.csv"))
+    for f in glob.glob(os.path.join(args.src, "trace_timed", "**", "*kernel_stats.csv"), recursive=True):
+        import shutil
+        shutil.copy(f, os.path.join(args.out, "kernel_stats_timed_mode.csv"))
     json.dump(d, open(path, "w"), indent=1)
     print(k, d[args.workload])
