@@ -14,6 +14,7 @@
 #   gpurun -- bash tools/gpu.sh shares <tag>                      # rank 0's share of N = 2, 4, 8 under PMC
 #                                                                  # (tools/gpu_share_pmc.sh) for the N > 1 roofline
 #   gpurun -- bash tools/gpu.sh tile <tag> [tile_scaling.py args] # per-rank share timing on one GPU
+#   gpurun -- bash tools/gpu.sh abi <tag>                         # the reference ABI's PCIe-inclusive rate
 # Summaries for profiles/: python tools/traffic_summary.py / tools/pmc_summary.py / tools/lane_weighted.py.
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
@@ -100,6 +101,10 @@ shares)
   bash tools/gpu_share_pmc.sh > $T/share_pmc.log 2>&1 || exit $?; tail -20 $T/share_pmc.log ;;
 tile)
   timeout -k 10 900 python3 tools/tile_scaling.py "$@" > $T/tile.json 2> $T/tile.err || exit $?; cat $T/tile.json ;;
+abi)
+  timeout -k 10 300 python3 tools/abi_rate.py > $T/abi_rate.json 2> $T/abi_rate.err || exit $?; cat $T/abi_rate.json
+  timeout -k 10 300 python3 tools/abi_rate.py --moving > $T/abi_rate_moving.json 2> $T/abi_rate_moving.err || exit $?
+  cat $T/abi_rate_moving.json ;;
 *)
   echo "unknown step $STEP"; exit 2 ;;
 esac
