@@ -120,6 +120,17 @@ def test_scene_loader_and_bvh_builders(driver, tmp_path, name):
         run(driver, "scene", root, p, *args[2:])
 
 
+@pytest.mark.parametrize("name", ["vanille", "vanille_nude", "subsurface_scattering_s", "dinosaur",
+                                  "c5_vanille_gallery"])
+def test_scene_loader_on_reference_assets(driver, tmp_path, name):
+    """The reference's own larger assets (tests/golden/ref_assets.tar.xz: vanille's 15-shape OBJ and 1024^2 TGA maps,
+    the cups, the sponza RGBA/RGB specular maps, the lobby BMP faces) through the loader and every builder under
+    ASan/UBSan, with the background override the GPU tests use."""
+    root = make_root(tmp_path, assets=True)
+    out = run(driver, "scene", root, root / "res" / "scene" / f"{name}.json", "res\\texture\\lobby", "bmp")
+    assert out.count(": rc") == 0, out
+
+
 def test_bvh_builders_on_degenerate_triangles(driver):
     for seed in (1, 2, 3):
         run(driver, "bvh", seed)
