@@ -348,10 +348,13 @@ def main() -> int:
     # their launches already follow each other on a context.
     wl = Workload(args.workload)
     # At 8 waves (profiles/r04/group/group_size_n2_n4.txt) 8 per launch beats 4 at N = 2 too (2.595-2.605 vs
-    # 2.653-2.659 ms per frame); 10 per launch is 1-3 % faster still at N = 2 and 4 over a 20-frame run (two
-    # launches of 10), but that is the driver's step count, not a property of the renderer: 8 everywhere.
+    # 2.653-2.659 ms per frame). The tail is paid per launch and lasts about 1 ms whatever the share (the last
+    # paths in flight), so a rank's launch carries 8 whole frames' units at every N: G = 8 N frames of a 1/N
+    # share (round 5, profiles/r05/group_n/: rank 0's 8-way share over 20 frames 0.721 ms per frame with 8 per
+    # launch, 0.679 with all 20 in one launch, 0.636 with 40 over 40 frames; 4-way 1.310 -> 1.272). At N = 1
+    # it stays 8 (8 + 8 + 4 over the driver's 20 steps); the launch never holds more frames than the run has.
     group = int(os.environ.get("PT_BENCH_GROUP", "0")) or (
-        1 if heavy or args.workload == "c1" or wl.spp > 8 else 8)
+        1 if heavy or args.workload == "c1" or wl.spp > 8 else 8 * world)
     inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or (
         2 if group > 1 else 3 if world == 1 else 5)
     grid_share = int(os.environ.get("PT_BENCH_GRID_SHARE", "0")) or (
@@ -368,8 +371,9 @@ def main() -> int:
         q.upload(scene, cfg)
         rs.append(q)
         if group > 1:
-            frames.append(pt.FrameGroup(q, width, height, group, dist if distributed else None, BAND_ROWS,
-                                        device=f"cuda:{local}"))
+            # buffers for the most frames one launch of this run holds (the warm-up's or the timed run's)
+            frames.append(pt.FrameGroup(q, width, height, max(1, min(group, max(args.steps, args.warmup))),
+                                        dist if distributed else None, BAND_ROWS, device=f"cuda:{local}"))
         else:
             frames.append(pt.TiledFrame(q, width, height, dist if distributed else None, BAND_ROWS,
                                         device=f"cuda:{local}" if distributed else None))

@@ -40,6 +40,9 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
 // frame: the frame of a pt_render_frames launch whose pass radiances are summed into image / image256
 hipError_t launch_accumulate(const LaunchParams* params_dev, int units, int first_pass, int batch_log2, int write_u8,
                              hipStream_t stream, int frame, float* image, uint8_t* image256);
+// every frame of a pt_render_frames launch at once; ptrs_dev: {images[0..frames), images256[0..frames)} on the device
+hipError_t launch_accumulate_frames(const LaunchParams* params_dev, int units, int first_pass, int batch_log2,
+                                    int write_u8, int frames, const uint64_t* ptrs_dev, hipStream_t stream);
 hipError_t launch_accumulate_one(const LaunchParams* params_dev, int unit_begin, int unit_end, int pass, int batch_log2,
                                  int j, int write_u8, const float* rad, hipStream_t stream);
 hipError_t launch_extend(const LaunchParams* P, bool gen, bool leaf1, bool stats, int depth, int pass, hipStream_t s);

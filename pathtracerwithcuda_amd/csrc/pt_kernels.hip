@@ -742,11 +742,9 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
 // pass after pass), then the 8-bit output of the batch's last pass.
 // frame: which frame copy of a pt_render_frames launch (0 otherwise)
 // frame's running sum `image` and 8-bit output `image256` (the launch's own, or a pt_render_frames frame's)
-__global__ __launch_bounds__(PT_BLOCK) void accumulate_kernel(const LaunchParams* __restrict__ P, int first_pass,
-                                                              int batch_log2, int write_u8, int frame,
-                                                              float* __restrict__ image, uint8_t* __restrict__ image256) {
-    const unsigned int lu = blockIdx.x * PT_BLOCK + threadIdx.x;
-    if (lu >= (unsigned int)P->til.unit_count) return;
+__device__ __forceinline__ void accumulate_unit(const LaunchParams* __restrict__ P, int first_pass, int batch_log2,
+                                                int write_u8, int frame, unsigned int lu, float* __restrict__ image,
+                                                uint8_t* __restrict__ image256) {
     const int pixel = unit_to_pixel(P->til, lu);
     const int batch = 1 << batch_log2;
     float* img = image + (size_t)pixel * 3;
@@ -768,6 +766,27 @@ __global__ __launch_bounds__(PT_BLOCK) void accumulate_kernel(const LaunchParams
     }
     img[0] = sum.x; img[1] = sum.y; img[2] = sum.z;
     if (write_u8 && image256) store_u8(P->cfg, sum, first_pass + batch - 1, image256 + (size_t)pixel * 3);
+}
+
+__global__ __launch_bounds__(PT_BLOCK) void accumulate_kernel(const LaunchParams* __restrict__ P, int first_pass,
+                                                              int batch_log2, int write_u8, int frame,
+                                                              float* __restrict__ image, uint8_t* __restrict__ image256) {
+    const unsigned int lu = blockIdx.x * PT_BLOCK + threadIdx.x;
+    if (lu >= (unsigned int)P->til.unit_count) return;
+    accumulate_unit(P, first_pass, batch_log2, write_u8, frame, lu, image, image256);
+}
+
+// Every frame of a pt_render_frames launch in one launch (blockIdx.y = frame): frame f's running sum and 8-bit
+// output are images[f] and images256[f] of a device table of 2 x frames pointers (images256[f] may be null).
+__global__ __launch_bounds__(PT_BLOCK) void accumulate_frames_kernel(const LaunchParams* __restrict__ P, int first_pass,
+                                                                     int batch_log2, int write_u8, int frames,
+                                                                     const uint64_t* __restrict__ ptrs) {
+    const unsigned int lu = blockIdx.x * PT_BLOCK + threadIdx.x;
+    if (lu >= (unsigned int)P->til.unit_count) return;
+    const int f = (int)blockIdx.y;
+    float* image = reinterpret_cast<float*>(ptrs[f]);
+    uint8_t* image256 = reinterpret_cast<uint8_t*>(ptrs[frames + f]);
+    accumulate_unit(P, first_pass, batch_log2, write_u8, f, lu, image, image256);
 }
 
 // One pass of a batched launch added into the running sum: pass `pass` is slot j of every unit's run of
@@ -1168,6 +1187,15 @@ hipError_t launch_accumulate(const LaunchParams* params_dev, int units, int firs
     if (units <= 0) return hipSuccess;
     hipLaunchKernelGGL(accumulate_kernel, dim3((units + PT_BLOCK - 1) / PT_BLOCK), dim3(PT_BLOCK), 0, stream,
                        params_dev, first_pass, batch_log2, write_u8, frame, image, image256);
+    return hipGetLastError();
+}
+
+hipError_t launch_accumulate_frames(const LaunchParams* params_dev, int units, int first_pass, int batch_log2,
+                                    int write_u8, int frames, const uint64_t* ptrs_dev, hipStream_t stream) {
+    if (units <= 0 || frames <= 0) return hipSuccess;
+    if (frames > 65535) return hipErrorInvalidValue;  // gridDim.y
+    hipLaunchKernelGGL(accumulate_frames_kernel, dim3((units + PT_BLOCK - 1) / PT_BLOCK, frames), dim3(PT_BLOCK), 0,
+                       stream, params_dev, first_pass, batch_log2, write_u8, frames, ptrs_dev);
     return hipGetLastError();
 }
 

@@ -1106,9 +1106,16 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
 // pt_render_frames: `frames` frames of the same passes, frame f through cams[f] into images[f] (and
 // images256[f]). With pass_kernel_u, one launch per batch of passes takes every frame's units (frame f's
 // are f * units_per_frame + its units), so the frames share one launch's start and tail instead of each
-// paying its own; its accumulate launches then sum each frame's pass radiances into that frame's image.
+// paying its own; one accumulate launch per batch then sums each frame's pass radiances into that frame's image.
 // Otherwise (the wavefront schedule, pass_kernel) the frames render one after another on the context.
 // Either way frame f is bit-identical to pt_render_passes of cams[f] on images[f].
+// Units (pixel x pass x frame) of one pt_render_frames launch at most. The kernel numbers them in 32-bit
+// unsigned arithmetic (work heads, which overshoot their region by at most a chunk per wave; the generation
+// ring), so 2^30 leaves a wide margin; pass_rad then takes 12 B per unit, 12.9 GB at the limit. A tiled share
+// renders many frames per launch (bench.py: 8 whole frames' units per launch at every rank count), so a
+// 1/8 share of 20 1080p frames (41 M units) and the whole 20 frames (332 M) are one launch each.
+constexpr long long kMaxFrameLaunchUnits = 1ll << 30;
+
 int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, const pt_configuration* config,
                   int first_pass, int pass_count, int write_u8, float* const* images, uint8_t* const* images256) {
     LaunchParams lp;
@@ -1135,19 +1142,31 @@ int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, con
         return rc;
     }
     const int units = ctx->tiling.unit_count;
-    if ((long long)units * frames > (1ll << 28)) { set_error("too many frames for one launch"); return PT_E_ARG; }
+    if ((long long)units * frames > kMaxFrameLaunchUnits) { set_error("too many frames for one launch"); return PT_E_ARG; }
+    if (frames > 65535) { set_error("more than 65535 frames in one launch"); return PT_E_ARG; }  // the accumulate's gridDim.y
+    // one upload: the frames' cameras, then the accumulate's table of image pointers {images, images256}
+    const size_t cam_bytes = ((size_t)frames * sizeof(DevCamera) + 7) & ~(size_t)7;
+    const size_t table_bytes = cam_bytes + (size_t)frames * 2 * sizeof(uint64_t);
     if (ctx->cams_cap < frames) {
         if (ctx->cams) (void)hipFree(ctx->cams);
         ctx->cams = nullptr;
         ctx->cams_cap = 0;
-        PT_HIP(hipMalloc(&ctx->cams, (size_t)frames * sizeof(DevCamera)));
+        PT_HIP(hipMalloc(&ctx->cams, table_bytes));
         ctx->cams_cap = frames;
     }
-    std::vector<DevCamera> dc((size_t)frames);
-    for (int f = 0; f < frames; f++) dc[(size_t)f] = to_dev(cams[f]);
-    PT_HIP(hipMemcpyAsync(ctx->cams, dc.data(), dc.size() * sizeof(DevCamera), hipMemcpyHostToDevice, ctx->stream));
+    std::vector<unsigned char> host(table_bytes, 0);
+    for (int f = 0; f < frames; f++) {
+        const DevCamera c = to_dev(cams[f]);
+        std::memcpy(host.data() + (size_t)f * sizeof(DevCamera), &c, sizeof(DevCamera));
+        const uint64_t pi = (uint64_t)(uintptr_t)images[f];
+        const uint64_t p8 = (uint64_t)(uintptr_t)(images256 ? images256[f] : nullptr);
+        std::memcpy(host.data() + cam_bytes + (size_t)f * 8, &pi, 8);
+        std::memcpy(host.data() + cam_bytes + (size_t)(frames + f) * 8, &p8, 8);
+    }
+    PT_HIP(hipMemcpyAsync(ctx->cams, host.data(), table_bytes, hipMemcpyHostToDevice, ctx->stream));
+    const uint64_t* ptrs_dev = reinterpret_cast<const uint64_t*>(reinterpret_cast<const unsigned char*>(ctx->cams) + cam_bytes);
     int most = 1;
-    while (most * 2 <= max_pass_batch() && (long long)units * most * 2 * frames <= (1ll << 28)) most *= 2;
+    while (most * 2 <= max_pass_batch() && (long long)units * most * 2 * frames <= kMaxFrameLaunchUnits) most *= 2;
     const size_t need = (size_t)units * (size_t)most * (size_t)frames * 12;
     if (need > ctx->pass_rad_bytes) {
         if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
@@ -1175,9 +1194,7 @@ int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, con
         PT_HIP(launch_pass(ctx->params, pc, first, lg, w8, g, pass_lds_bytes(ctx), ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         if ((rc = ev_begin(ctx, 3)) != PT_OK) return rc;
-        for (int f = 0; f < frames; f++)
-            PT_HIP(launch_accumulate(ctx->params, units, first, lg, w8, ctx->stream, f, images[f],
-                                     images256 ? images256[f] : nullptr));
+        PT_HIP(launch_accumulate_frames(ctx->params, units, first, lg, w8, frames, ptrs_dev, ctx->stream));
         if ((rc = ev_end(ctx)) != PT_OK) return rc;
         i += b;
     }

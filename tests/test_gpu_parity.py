@@ -411,6 +411,38 @@ def test_metric_frames_grouped_as_the_bench_times_them(bench_gpu):
         assert_bitwise(imgs8[f].cpu().numpy().reshape(-1, 3), ref8, f"grouped frame {f} 8-bit")
 
 
+def test_twenty_frames_in_one_launch_beyond_2e28_units(bench_gpu):
+    """The launch bench.py times at N >= 4 (8 N frames of a 1/N share per launch, so the driver's 20 steps are
+    one launch): here the whole frame, 20 metric frames of 8 passes in ONE pass launch, 331.8 M units, past
+    round 4's 2^28-unit cap, which split such a group into two launches of 4 passes. Frames 0, 9 and 19 (each
+    through its own orbiting camera) equal the same camera's frame rendered alone by pt_render_passes, float
+    and 8-bit, bit for bit; that single-frame path is the oracle-checked one
+    (test_metric_frame_at_the_bench_launch_shape)."""
+    import torch
+
+    import bench
+    wl = bench.Workload("metric")
+    r = bench_gpu
+    r.upload(wl.scene, wl.cfg)
+    r.setup_frame(wl.width, wl.height)
+    cams = [pt.camera(wl.width, wl.height, yaw=0.02 * i, **BENCH_CAM) for i in range(20)]
+    n = wl.width * wl.height * 3
+    assert n // 3 * 8 * len(cams) > (1 << 28)
+    imgs = [torch.zeros(n, dtype=torch.float32, device="cuda:0") for _ in cams]
+    imgs8 = [torch.zeros(n, dtype=torch.uint8, device="cuda:0") for _ in cams]
+    r.stats_reset()
+    r.render_frames(cams, wl.cfg, imgs, imgs8, 1, 8, write_u8=2)
+    r.synchronize()
+    assert r.kernel_time_kind(0)[1] == 1, "one pass launch for the twenty frames"
+    for f in (0, 9, 19):
+        r.render(cams[f], wl.cfg, 1, 8, write_u8=2)
+        r.synchronize()
+        solo, solo8 = r.download()
+        assert_bitwise(imgs[f].cpu().numpy().reshape(-1, 3), np.asarray(solo).reshape(-1, 3), f"frame {f} float")
+        assert_bitwise(imgs8[f].cpu().numpy().reshape(-1, 3), np.asarray(solo8).reshape(-1, 3), f"frame {f} 8-bit")
+    del imgs, imgs8
+
+
 def test_c2_diffuse_mesh_frame(bench_gpu):
     """BASELINE config C2 as its own workload (bench.py --workload c2): the Cornell walls and light with
     the 70k-triangle mesh, diffuse only, no spheres, 1280x720, 8 passes at the bench launch shape. Whole

@@ -12,11 +12,11 @@ mkdir -p gpurun_out/$TAG
 timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --save-image gpurun_out/$TAG/n1.png > gpurun_out/$TAG/b1.json 2>/dev/null || exit $?
 run() {  # name ranks port extra-env...
   m=$1; n=$2; port=$3; shift 3
-  env "$@" PT_BENCH_BACKEND=gloo PT_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $port bench.py --gpus $n --steps 5 --warmup 1 --save-image gpurun_out/$TAG/$m.png > gpurun_out/$TAG/$m.json 2> gpurun_out/$TAG/$m.err || exit $?
+  env "$@" PT_BENCH_BACKEND=gloo PT_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $port bench.py --gpus $n --steps ${S:-5} --warmup 1 --save-image gpurun_out/$TAG/$m.png > gpurun_out/$TAG/$m.json 2> gpurun_out/$TAG/$m.err || exit $?
   python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], 'ranks: image_matches_1gpu', d['config']['image_matches_1gpu'], 'frames per launch', d['config']['frames_per_launch'], d['value'], 'Mrays/s')" gpurun_out/$TAG/$m.json $n
   cmp gpurun_out/$TAG/n1.png gpurun_out/$TAG/$m.png || exit 4
 }
-# b*: one frame per launch (PT_BENCH_GROUP=1); g*: the default frame groups at N > 1 (8 frames per launch,
+# b*: one frame per launch (PT_BENCH_GROUP=1); g*: the default frame groups at N > 1 (8 N frames per launch,
 # one collective per group): 5 steps = one launch of 5 frames
 run b2 2 29533 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=1
 run b3 3 29534 PT_FRAME_COLLECTIVE=reduce PT_BENCH_GROUP=1
@@ -26,4 +26,7 @@ run g2 2 29537 PT_FRAME_COLLECTIVE=reduce
 run g3 3 29538 PT_FRAME_COLLECTIVE=gather
 run g4 4 29539 PT_FRAME_COLLECTIVE=gather
 run g8 8 29540 PT_FRAME_COLLECTIVE=gather
+# the driver's 20 steps: with G = 8 N frames per launch, one launch of 20 frames at N = 4 and 8
+S=20 run g4s20 4 29541 PT_FRAME_COLLECTIVE=gather
+S=20 run g8s20 8 29542 PT_FRAME_COLLECTIVE=reduce
 echo "saved images identical to the 1-GPU image"
