@@ -525,7 +525,7 @@ def main() -> int:
         bytes_per_launch = extend_bytes(counts, scene.view.sphere_num) / world / frame_launches
         kernel_name = "extend_kernel<LEAF1=true,STATS=false>"
     workload = wl.key
-    key = workload + ("" if schedule == "persistent" else "/wavefront")
+    key = workload + ("" if schedule == "persistent" else "/wavefront") + ("/medium_bound" if args.medium_bound else "")
     # N > 1: rank 0's share profiled on its own (tools/gpu_share_pmc.sh, "<key>/tiled<N>"); otherwise the
     # whole 1-GPU frame's profile, of which a rank of N runs 1/N
     prof = load_profile(f"{key}/tiled{world}") if world > 1 else {}

@@ -7,6 +7,7 @@
 #        BENCH_ARGS (default: the driver's --steps 20 --warmup 5) and TESTS=1 (parity of each lib first)
 #   gpurun -- bash tools/gpu.sh workloads <tag>                   # the metric line + c1..c5 (+ c4 --medium-bound)
 #   gpurun -- bash tools/gpu.sh profile <tag>                     # rocprof traces + PMC passes + PT_UPROF + PT_DUP
+#   gpurun -- bash tools/gpu.sh wlprofile <tag>                   # c1..c5 (+ c4 --medium-bound): trace + PMC passes
 #   gpurun -- bash tools/gpu.sh orbit <tag>                       # static vs per-frame camera, with and without groups
 #   gpurun -- bash tools/gpu.sh rccl <tag>                        # bench --rccl + its rocprofv3 RCCL API trace
 #   gpurun -- bash tools/gpu.sh rehearsal <tag>                   # N = 2..8 gloo ranks on the one GPU (bench.py's
@@ -83,6 +84,22 @@ profile)
   timeout -k 10 120 python3 tools/uprof.py metric > $T/uprof_metric.json 2> $T/uprof_metric.err || exit $?
   if [ -d $PKG/lib_dup1 ]; then bash tools/gpu_dup.sh $TAG/dup > $T/dup.log 2>&1 || exit $?; tail -4 $T/dup.log; fi
   echo profile done ;;
+wlprofile)
+  # the other configurations' roofline inputs, each workload's solo launch (one frame per launch, one in flight):
+  # kernel trace, FETCH_SIZE, WRITE_SIZE and SQ passes; then per workload
+  #   python tools/traffic_summary.py gpurun_out/<tag>/<w> profiles/<round>/workloads/<w> --workload <key> --kernel "pass_kernel_u<"
+  export PT_BENCH_INFLIGHT=1 PT_BENCH_GROUP=1
+  for w in ${WORKLOADS:-c1 c2 c3 c4 c4mb c5}; do
+    a="--workload ${w%mb} --no-cpu-baseline"; [ "$w" = c4mb ] && a="$a --medium-bound"
+    st="--steps 3 --warmup 1"; sp="--steps 1 --warmup 0"
+    case $w in c1) st="--steps 40 --warmup 2"; sp="--steps 4 --warmup 0" ;; c5) st="--steps 1 --warmup 0" ;; esac
+    mkdir -p $T/$w
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $T/$w/trace -o run -- python3 bench.py $a $st > $T/$w/trace.log 2>&1 || exit $?
+    timeout -s KILL 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $T/$w/pmc_fetch -o run -- python3 bench.py $a $sp > $T/$w/pmc_fetch.log 2>&1 || exit $?
+    timeout -s KILL 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $T/$w/pmc_write -o run -- python3 bench.py $a $sp > $T/$w/pmc_write.log 2>&1 || exit $?
+    timeout -s KILL 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $T/$w/pmc_sq -o run -- python3 bench.py $a $sp > $T/$w/pmc_sq.log 2>&1 || exit $?
+    echo "$w profiled"
+  done ;;
 orbit)
   for r in 1 2; do
     for v in "" "--orbit 0.01"; do for g in 8 1; do
