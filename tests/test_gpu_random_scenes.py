@@ -133,3 +133,50 @@ def test_random_scene_frame_equals_the_oracle(renderers, seed):
             assert np.array_equal(img8.reshape(-1, 3), ref8.reshape(-1, 3)), f"seed {seed} {schedule}: 8-bit differs"
     finally:
         sc.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(96))
+def test_random_scene_frame_groups_equal_the_oracle(renderers, seed):
+    """pt_render_frames (the MULTI instances, one per scene feature set) on the same random scenes: 2-5 frames,
+    each through its own camera, one launch per batch of passes, with a random band share (rows of one band
+    index of 1-3, bands of 1-8 rows) and grid share. Every frame's owned rows against the oracle's frame of its
+    camera, bit for bit; rows outside the share keep the caller's fill value."""
+    import torch
+
+    sc, cfg, cam0, first, count = random_case(10_000 + seed)
+    rng = np.random.default_rng(20_000 + seed)
+    try:
+        W, H = int(cam0.resolution[0]), int(cam0.resolution[1])
+        cams = [cam0] + [pt.camera(W, H, yaw=float(rng.uniform(-3.1, 3.1)), pitch=float(rng.uniform(-1.0, 1.0)),
+                                   radius=float(rng.uniform(3.0, 14.0))) for _ in range(int(rng.integers(1, 5)))]
+        band_rows, band_count = int(rng.choice([1, 3, 8])), int(rng.integers(1, 4))
+        band_index = int(rng.integers(0, band_count))
+        r = renderers["persistent"]
+        r.upload(sc, cfg)
+        r.setup_frame(W, H)
+        r.set_tiling(band_rows, band_count, band_index)
+        r.set_grid_share(int(rng.choice([100, 100, 45, 10])))
+        try:
+            n = W * H * 3
+            imgs = [torch.full((n,), 7.0, dtype=torch.float32, device="cuda:0") for _ in cams]
+            imgs8 = [torch.zeros((n,), dtype=torch.uint8, device="cuda:0") for _ in cams]
+            if first > 1:
+                r.render_frames(cams, cfg, imgs, imgs8, 1, first - 1, write_u8=0)
+            r.render_frames(cams, cfg, imgs, imgs8, first, count, write_u8=2)
+            r.synchronize()
+        finally:
+            r.set_tiling(1, 1, 0)
+            r.set_grid_share(100)
+        rows = [y for y in range(H) if (y // band_rows) % band_count == band_index]
+        other = [y for y in range(H) if y not in rows]
+        for f, cam in enumerate(cams):
+            ref, ref8, _ = oracle.render(sc.view, cam, cfg, 1, first - 1 + count)
+            img = imgs[f].cpu().numpy().reshape(H, W, 3)
+            a, b = img[rows].reshape(-1, 3), ref.reshape(H, W, 3)[rows].reshape(-1, 3)
+            same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+            assert same.all(), f"seed {seed} frame {f}: {int((~same).any(axis=1).sum())} pixels differ"
+            assert np.array_equal(imgs8[f].cpu().numpy().reshape(H, W, 3)[rows], ref8.reshape(H, W, 3)[rows])
+            assert (img[other] == 7.0).all(), f"seed {seed} frame {f}: rows outside the share written"
+    finally:
+        sc.close()
