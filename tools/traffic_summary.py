@@ -59,19 +59,25 @@ if args.workload:
     rec = d[args.workload]
     # the timed mode's kernel (frame groups: the MULTI instance), from the pmc_sq_group8 pass of tools/gpu.sh
     # profile (tools/share_render.py --group 8: one launch of 8 frames), VALU per frame
-    multi = {}
-    for f in glob.glob(os.path.join(args.src, "pmc_sq_group8", "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == "SQ_INSTS_VALU" and "pass_kernel_u<" in r["Kernel_Name"] and ", true>" in r["Kernel_Name"]:
-                multi.setdefault(r["Kernel_Name"].split("(")[0], []).append(float(r["Counter_Value"]))
-    if multi:
-        mk, mv = next(iter(multi.items()))
-        rec["valu_insts_per_frame_timed"] = round(sum(mv) / len(mv) / 8)
-        rec["valu_insts_per_frame_timed_source"] = (f"{os.path.relpath(args.out)}/pmc_sq_group8.json: SQ_INSTS_VALU of "
-                                                    f"{mk} (the MULTI instance the timed launches run) over one "
-                                                    "8-frame launch / 8")
-        json.dump({mk: {"SQ_INSTS_VALU_per_launch": sum(mv) / len(mv), "frames_per_launch": 8}},
-                  open(os.path.join(args.out, "pmc_sq_group8.json"), "w"), indent=1)
+    # pmc_sq_group<G>: one launch of G frames (G = 8 for the 1-GPU frame; min(8 N, 20) for a 1/N share, as the
+    # driver's 20 steps run it)
+    for gdir in sorted(glob.glob(os.path.join(args.src, "pmc_sq_group*"))):
+        if not os.path.isdir(gdir):
+            continue
+        G = int(os.path.basename(gdir)[len("pmc_sq_group"):])
+        multi = {}
+        for f in glob.glob(os.path.join(gdir, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if r["Counter_Name"] == "SQ_INSTS_VALU" and "pass_kernel_u<" in r["Kernel_Name"] and ", true>" in r["Kernel_Name"]:
+                    multi.setdefault(r["Kernel_Name"].split("(")[0], []).append(float(r["Counter_Value"]))
+        if multi:
+            mk, mv = next(iter(multi.items()))
+            rec["valu_insts_per_frame_timed"] = round(sum(mv) / len(mv) / G)
+            rec["valu_insts_per_frame_timed_source"] = (f"{os.path.relpath(args.out)}/pmc_sq_group{G}.json: SQ_INSTS_VALU "
+                                                        f"of {mk} (the MULTI instance the timed launches run) over one "
+                                                        f"{G}-frame launch / {G}")
+            json.dump({mk: {"SQ_INSTS_VALU_per_launch": sum(mv) / len(mv), "frames_per_launch": G}},
+                      open(os.path.join(args.out, f"pmc_sq_group{G}.json"), "w"), indent=1)
     # the solo launch's average duration in rocprofv3's kernel trace (one frame in flight)
     for f in glob.glob(os.path.join(args.src, "trace", "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
