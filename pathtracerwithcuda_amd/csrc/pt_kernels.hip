@@ -692,6 +692,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     opaque(w2); opaque(l2); opaque(t2); opaque(a2); opaque(b2); opaque(c2);
                 }
                 // a leaf whose box passes: the lane parks with its triangle, which came with the step's records
+                if (PT_WALK_PRIO) __builtin_amdgcn_s_setprio(PT_WALK_PRIO);  // until the step's loads issue (pt_path.h)
                 if (walk_box_inline(rn, ps.o, inv, w, ptri, pta, ptb, ptc)) mode = LANE_TRI;
             }
             // leaf triangles are tested in batches of at least tri_min lanes (or when no lane can walk on,

@@ -450,6 +450,17 @@ __device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, 
     return chain_test<CHAIN>(r, o, inv, w, tri);
 }
 
+// Issue priority of a walk step from its start until its four loads are issued (s_setprio; pass_kernel_u raises
+// it before walk_box_inline, which drops it to 0 right after the loads). Waves that stand ready to send a step's
+// loads then win the SIMD's issue arbitration over waves in box tests, triangle batches or shading (31 % of wave
+// cycles are issue stalls: SQ_WAIT_INST_ANY, profiles/r05/prio/), so the loads, the dependent chain that bounds
+// the walk, start sooner. Scheduling only: the same instructions on the same values. Measured
+// (profiles/r05/prio/ab.txt): metric 14547-14563 vs 14379-14384 Mrays/s, C4 +5.1 %, C5 +3.1 %, C3 +0.7 %; levels
+// 1 and 2 gain about as much; priority held through the whole step loses (14282-14298).
+#ifndef PT_WALK_PRIO
+#define PT_WALK_PRIO 3
+#endif
+
 // The two-record step over the inline-leaf layout (pass_kernel_u, one triangle per leaf): a leaf is
 // two records, its box record {lo, e2.z} {hi, slot} followed by its triangle {v0, e1.x} {e1.y, e1.z,
 // e2.x, e2.y}; an internal record keeps {lo, skip} {hi, -1}. A leaf's skip is always the record after
@@ -462,7 +473,13 @@ __device__ __forceinline__ bool walk_box_inline(const __amdgpu_buffer_rsrc_t rn,
                                                 float4& a, float4& e1, float4& e2) {
     const float4 lo0 = bload(rn, w.pos * 32), hi0 = bload(rn, w.pos * 32 + 16);
     const float4 lo1 = bload(rn, w.pos * 32 + 32), hi1 = bload(rn, w.pos * 32 + 48);
-    asm volatile("" ::"v"(lo1.w), "v"(hi1.w));  // one round trip for all four loads (chain_load)
+#if PT_WALK_PRIO
+    __builtin_amdgcn_s_setprio(0);  // the caller's raised issue priority ends once the step's loads are issued
+#endif
+    // one wait for all four loads (chain_load). Without it the compiler issues them in record order and tests
+    // the first record after two (vmcnt(2)): the same registers and −0.2–0.6 % (profiles/r05/prio/ab_nopin.txt),
+    // as the four 16-B pieces of one 64-B run return together
+    asm volatile("" ::"v"(lo1.w), "v"(hi1.w));
     // the triangle operands of a first-record leaf, assigned on every step (they are read only after a
     // park): a conditional assignment makes the compiler merge old and new values through copies
     const int slot0 = f2i(hi0.w);
