@@ -487,29 +487,50 @@ __device__ __forceinline__ bool walk_box_inline(const __amdgpu_buffer_rsrc_t rn,
     a = make_float4(lo1.x, lo1.y, lo1.z, 0.0f);
     e1 = make_float4(lo1.w, hi1.x, hi1.y, 0.0f);
     e2 = make_float4(hi1.z, hi1.w, lo0.w, 0.0f);
-    float entry;
-    if (box_hit(lo0, hi0, o, inv, &entry) && entry <= w.t) {
-        if (slot0 >= 0) return true;
-        w.pos++;
-        const int slot1 = f2i(hi1.w);
-        if (box_hit(lo1, hi1, o, inv, &entry) && entry <= w.t) {
-            if (slot1 < 0) w.pos++;
-        } else {
-            w.pos = slot1 >= 0 ? w.pos + 2 : f2i(lo1.w);
-        }
-        return false;
-    }
-    w.pos = slot0 >= 0 ? w.pos + 2 : f2i(lo0.w);
-    return false;
+    // Both records' box tests always run and the next position is chosen by selects: the wave executed the
+    // second record's test whenever any lane needed it anyway, and the nested branches cost exec-mask SALU
+    // and branches on every step (31 % of wave cycles are issue stalls). Round 5: metric 14673-14700 vs
+    // 14537-14567 Mrays/s, C4 +1.7 %, C5 +1.1 %, C3 +-0 (profiles/r05/select/ab.txt).
+    float en0, en1;
+    const bool p0 = box_hit(lo0, hi0, o, inv, &en0) && en0 <= w.t;
+    const bool p1 = box_hit(lo1, hi1, o, inv, &en1) && en1 <= w.t;  // meaningful only when rec0 is internal
+    const bool leaf0 = slot0 >= 0, leaf1 = f2i(hi1.w) >= 0;
+    const int pos = w.pos;
+    int skip0 = f2i(lo0.w), skip1 = f2i(lo1.w);
+    asm("" : "+v"(skip0), "+v"(skip1));  // not loads, for the select-to-branch heuristic: the selects stay selects
+    // rec0 fails: skip it (a leaf's skip is the record after its triangle). rec0 is a passing leaf: park (the
+    // walk stays). rec0 is a passing internal record: rec1 is its left child; a passing leaf there ends the step
+    // on it (tested again next step with its triangle), a passing internal rec1 descends, a failing one is skipped
+    const int after1 = p1 ? (leaf1 ? pos + 1 : pos + 2) : (leaf1 ? pos + 3 : skip1);
+    w.pos = p0 ? (leaf0 ? pos : after1) : (leaf0 ? pos + 2 : skip0);
+    return p0 && leaf0;
 }
 
 // The leaf's triangle test (triangle.h:27-62, accepted when t > 0 && t < min_t, :128) with its records
 // already loaded, then the walk moves past the leaf.
-__device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri) {
+__device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri,
+                                              bool on = true) {
+#if defined(PT_TRI_SELECT) && PT_TRI_SELECT
+    // experiment: triangle_test's arithmetic without its early return, the hit taken by selects
+    v3 v0 = f4xyz(a), e1 = f4xyz(b), e2 = f4xyz(c);
+    v3 p = cross(d, e2);
+    float det = dot(e1, p);
+    float inv = rcp_exact(det);  // == 1.0f / det; not used when det == 0
+    v3 tv = o - v0;
+    v3 q = cross(tv, e1);
+    float t1 = dot(tv, p) * inv;
+    float t2 = dot(d, q) * inv;
+    float tt = dot(e2, q) * inv;
+    const bool hit = on && det != 0.0f && t1 >= 0.0f && t2 >= 0.0f && t1 + t2 <= 1.0f && tt > 0.0f && tt < w.t;
+    w.t = hit ? tt : w.t; w.t1 = hit ? t1 : w.t1; w.t2 = hit ? t2 : w.t2; w.tri = hit ? tri : w.tri;
+    w.pos += on ? 1 : 0;
+    return;
+#else
     float t, t1, t2;
     if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t) {
         w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
     }
+#endif
     w.pos++;
 }
 
