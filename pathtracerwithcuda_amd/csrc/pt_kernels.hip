@@ -646,17 +646,9 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         const __amdgpu_buffer_rsrc_t rn = make_rsrc(sc.nodes, sc.node_count * 32);
         // closest_hit's merge of a finished mesh walk (:443-454), then the next mesh or READY
         auto mesh_done = [&]() {
-#if defined(PT_MERGE_SELECT) && PT_MERGE_SELECT
-            {
-                const bool take = w.tri >= 0 && w.t < h.t;
-                h.t = take ? w.t : h.t; h.t1 = take ? w.t1 : h.t1; h.t2 = take ? w.t2 : h.t2;
-                h.prim = take ? w.tri : h.prim; h.type = take ? 2 : h.type;
-            }
-#else
             if (w.tri >= 0 && w.t < h.t) {
                 h.t = w.t; h.t1 = w.t1; h.t2 = w.t2; h.prim = w.tri; h.type = 2;
             }
-#endif
             bool more;
             int2 range = make_int2(0, 0);
             if (roots) {
@@ -709,15 +701,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             const unsigned long long pend = __ballot(mode == LANE_TRI);
             if (pend && (__popcll(pend) >= (unsigned int)tri_min || !__any(mode == LANE_WALK) || k == walk_steps - 1)) {
                 if (PROF) { prof[5]++; prof[6] += (unsigned long long)__popcll(pend); }
-#if defined(PT_TRI_SELECT) && PT_TRI_SELECT
-                // every lane runs the test (the wave issues it once either way); only parked lanes take its result
-                {
-                    const bool parked = mode == LANE_TRI;
-                    walk_tri_geom(pta, ptb, ptc, ps.o, ps.d, w, ptri, parked);
-                    w.pos += parked ? 1 : 0;  // past the leaf's triangle record too
-                    mode = parked ? LANE_WALK : mode;
-                }
-#else
                 if (mode == LANE_TRI) {
                     if (PT_DUP == 3) {
                         MeshWalk w2 = w; v3 o2 = ps.o, d2 = ps.d; float4 a2 = pta, b2 = ptb, c2 = ptc; int t2 = ptri;
@@ -729,7 +712,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     w.pos++;  // past the leaf's triangle record too
                     mode = LANE_WALK;
                 }
-#endif
             }
             // a lane whose mesh walk ended in this step (after a box or after its triangle) merges it and
             // starts the next mesh: one mesh_done site for both
