@@ -456,7 +456,8 @@ __device__ __forceinline__ bool walk_box_chain(const __amdgpu_buffer_rsrc_t rn, 
 // cycles are issue stalls: SQ_WAIT_INST_ANY, profiles/r05/prio/), so the loads, the dependent chain that bounds
 // the walk, start sooner. Scheduling only: the same instructions on the same values. Measured
 // (profiles/r05/prio/ab.txt): metric 14547-14563 vs 14379-14384 Mrays/s, C4 +5.1 %, C5 +3.1 %, C3 +0.7 %; levels
-// 1 and 2 gain about as much; priority held through the whole step loses (14282-14298).
+// 1 and 2 gain about as much; priority held through the whole step loses (14282-14298), and so does a middle
+// level (1 or 2) for the box tests after the loads issue (-1.3 %, profiles/r05/prio/ab_test_levels.txt).
 #ifndef PT_WALK_PRIO
 #define PT_WALK_PRIO 3
 #endif
