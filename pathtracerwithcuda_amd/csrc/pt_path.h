@@ -510,10 +510,21 @@ __device__ __forceinline__ bool walk_box_inline(const __amdgpu_buffer_rsrc_t rn,
 // The leaf's triangle test (triangle.h:27-62, accepted when t > 0 && t < min_t, :128) with its records
 // already loaded, then the walk moves past the leaf.
 __device__ __forceinline__ void walk_tri_geom(float4 a, float4 b, float4 c, v3 o, v3 d, MeshWalk& w, int tri) {
-    float t, t1, t2;
-    if (triangle_test(a, b, c, o, d, &t, &t1, &t2) && t > 0.0f && t < w.t) {
-        w.t = t; w.t1 = t1; w.t2 = t2; w.tri = tri;
-    }
+    // triangle_test's arithmetic without its early return on det == 0 (1/det is then not used), the hit taken by
+    // selects: the batch's instructions are the same, its exec-mask branches go (round 5: metric +0.6-1.0 %, C4
+    // +0.8 %, C5 +0.5 %; profiles/r05/select/ab_tri_inside.txt). Running the test on every lane instead, with the
+    // batch's own exec branch removed too, lost 1.5 % (ab_tri_merge.txt).
+    v3 v0 = f4xyz(a), e1 = f4xyz(b), e2 = f4xyz(c);
+    v3 p = cross(d, e2);
+    float det = dot(e1, p);
+    float inv = rcp_exact(det);  // == 1.0f / det
+    v3 tv = o - v0;
+    v3 q = cross(tv, e1);
+    float t1 = dot(tv, p) * inv;
+    float t2 = dot(d, q) * inv;
+    float tt = dot(e2, q) * inv;
+    const bool hit = det != 0.0f && t1 >= 0.0f && t2 >= 0.0f && t1 + t2 <= 1.0f && tt > 0.0f && tt < w.t;
+    w.t = hit ? tt : w.t; w.t1 = hit ? t1 : w.t1; w.t2 = hit ? t2 : w.t2; w.tri = hit ? tri : w.tri;
     w.pos++;
 }
 
