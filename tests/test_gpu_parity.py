@@ -443,6 +443,29 @@ def test_twenty_frames_in_one_launch_beyond_2e28_units(bench_gpu):
     del imgs, imgs8
 
 
+def test_render_frames_refuses_launches_past_its_limits(bench_gpu):
+    """pt_render_frames' limits fail loudly before any work: more than 2^30 units (share pixels x passes x
+    frames, the kernel's 32-bit unit numbers) and more than 65535 frames (the accumulate launch's grid y)."""
+    import torch
+
+    sc = pt.cornell_scene(pt.torus_knot(20, 6), cube_length=8)
+    cfg = pt.configuration(max_tracer_depth=2)
+    r = bench_gpu
+    r.upload(sc, cfg)
+    img = torch.zeros(3, dtype=torch.float32, device="cuda:0")
+    r.setup_frame(1, 1)
+    cam = pt.camera(1, 1, **BENCH_CAM)
+    with pytest.raises(pt.PtError, match="65535 frames"):
+        r.render_frames([cam] * 65536, cfg, [img] * 65536, None, 1, 1, write_u8=0)
+    big = pt.camera(4096, 4096, **BENCH_CAM)
+    r.setup_frame(4096, 4096)
+    imgs = [torch.zeros(3, dtype=torch.float32, device="cuda:0")] * 65  # never written: refused first
+    assert 4096 * 4096 * 65 > (1 << 30)
+    with pytest.raises(pt.PtError, match="too many frames"):
+        r.render_frames([big] * 65, cfg, imgs, None, 1, 1, write_u8=0)
+    r.synchronize()
+
+
 def test_c2_diffuse_mesh_frame(bench_gpu):
     """BASELINE config C2 as its own workload (bench.py --workload c2): the Cornell walls and light with
     the 70k-triangle mesh, diffuse only, no spheres, 1280x720, 8 passes at the bench launch shape. Whole
