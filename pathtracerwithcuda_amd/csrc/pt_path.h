@@ -201,6 +201,13 @@ __device__ __forceinline__ float u8_unit(unsigned int b) {
     return fmaf(r, c, q);
 }
 
+// A bilinear lookup issues its four texel loads at raised wave priority, as a walk step does its node loads
+// (PT_WALK_PRIO below): round 5, C5 +0.2-0.35 %, C3 +0.25-0.37 %, metric +0.1-0.4 % (the sky's cube-map
+// lookups), profiles/r05/prio/ab_tex.txt. Scheduling only.
+#ifndef PT_TEX_PRIO
+#define PT_TEX_PRIO 3
+#endif
+
 // One RGBA8 texel as a packed word; channels are converted one at a time where they are used, so a
 // bilinear sample holds four words instead of twelve floats.
 __device__ __forceinline__ unsigned int texel_raw(const uint8_t* px, int idx) {
@@ -220,8 +227,14 @@ __device__ __forceinline__ v3 sample_rgba8(const uint8_t* px, int w, int h, floa
         int cy = (int)clampf(ceilf(yr), 0.0f, (float)(h - 1));
         float lr = xr - floorf(xr);
         float bt = yr - floorf(yr);
+#if PT_TEX_PRIO
+        __builtin_amdgcn_s_setprio(PT_TEX_PRIO);  // until the four texel loads issue (PT_TEX_PRIO)
+#endif
         const unsigned int t0 = texel_raw(px, fy * w + fx), t1 = texel_raw(px, fy * w + cx);
         const unsigned int t2 = texel_raw(px, cy * w + fx), t3 = texel_raw(px, cy * w + cx);
+#if PT_TEX_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         float o[3];
 #pragma unroll
         for (int c = 0; c < 3; c++)  // lerp(lerp(c0, c1, lr), lerp(c2, c3, lr), bt), one channel at a time
@@ -246,7 +259,13 @@ __device__ __forceinline__ v3 sample_f4(const float4* px, int w, int h, float au
         int cy = (int)clampf(ceilf(yr), 0.0f, (float)(h - 1));
         float lr = xr - floorf(xr);
         float bt = yr - floorf(yr);
+#if PT_TEX_PRIO
+        __builtin_amdgcn_s_setprio(PT_TEX_PRIO);  // until the four texel loads issue (PT_TEX_PRIO)
+#endif
         const float4 t0 = px[fy * w + fx], t1 = px[fy * w + cx], t2 = px[cy * w + fx], t3 = px[cy * w + cx];
+#if PT_TEX_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         return mk3(lerp1(lerp1(t0.x, t1.x, lr), lerp1(t2.x, t3.x, lr), bt),
                    lerp1(lerp1(t0.y, t1.y, lr), lerp1(t2.y, t3.y, lr), bt),
                    lerp1(lerp1(t0.z, t1.z, lr), lerp1(t2.z, t3.z, lr), bt));
