@@ -153,7 +153,8 @@ class TiledFrame:
 class FrameGroup:
     """`frames` frames per launch on this rank's bands (pt_render_frames), then ONE collective for all of
     them: the group's float images are one [frames, height * width * 3] buffer, so the gather moves every
-    frame's rows in one call (the reduce sums the whole stack). The frames share one pass launch's start
+    frame's rows in one call (with a second for the ranks' own 8-bit rows; the reduce sums the whole stack and
+    rank 0 writes the 8-bit images). The frames share one pass launch's start
     and tail instead of each paying its own, which is most of a small share's cost. Frame f
     of a launch is bit-identical to a TiledFrame's frame through the same camera.
 
@@ -189,10 +190,15 @@ class FrameGroup:
             most = max(len(rw) for rw in self.rows)
             self.most = most
             self.part = torch.zeros(frames, most, width, 3, dtype=torch.float32, device=device)
-            self.parts = None
+            # the gather also moves each rank's 8-bit rows, written by its own accumulate launch (the same per-pixel
+            # gamma function as a finalize on rank 0, which then has none to run): 3 B more per pixel on the links
+            self.part8 = torch.zeros(frames, most, width, 3, dtype=torch.uint8, device=device)
+            self.parts = self.parts8 = None
             if self.rank == 0:
                 self.landing = torch.zeros(self.world, frames, most, width, 3, dtype=torch.float32, device=device)
+                self.landing8 = torch.zeros(self.world, frames, most, width, 3, dtype=torch.uint8, device=device)
                 self.parts = list(self.landing.unbind(0))
+                self.parts8 = list(self.landing8.unbind(0))
                 self.src_rows, self.dst_rows = _placement(self.rows, most, device)
         if self.stack.is_cuda and hasattr(renderer, "stream_handle"):
             self.stream = torch.cuda.ExternalStream(renderer.stream_handle(), device=self.stack.device)
@@ -208,7 +214,8 @@ class FrameGroup:
 
     def launch(self, cams, cfg, spp: int) -> None:
         """Queues passes 1..spp of len(cams) <= frames frames (frame f through cams[f]), then (world > 1) the
-        group's one collective and rank 0's 8-bit outputs, in order on the renderer's stream."""
+        group's collective (gather: the float and the 8-bit rows of every rank; reduce: the float stack, then rank
+        0's 8-bit outputs), in order on the renderer's stream."""
         n = len(cams)
         if not 1 <= n <= self.frames:
             raise ValueError(f"1..{self.frames} cameras per launch, got {n}")
@@ -220,22 +227,29 @@ class FrameGroup:
         with self._on_stream():
             if self.collective == "reduce":
                 self.stack[:n].zero_()  # rows outside this rank's bands must be zero for the reduce
-            self.r.render_frames(list(cams), cfg, self.images[:n], None, 1, spp, write_u8=0)
+                self.r.render_frames(list(cams), cfg, self.images[:n], None, 1, spp, write_u8=0)
+                if self.stream is None:
+                    self.r.synchronize()
+                self.dist.reduce(self.stack, dst=0)  # the one collective of the group
+                if self.rank == 0:
+                    for f in range(n):
+                        self.r.finalize_u8_image(cfg, spp, self.images[f], self.images8[f])
+                return
+            self.r.render_frames(list(cams), cfg, self.images[:n], self.images8[:n], 1, spp, write_u8=2)
             if self.stream is None:
                 self.r.synchronize()
-            if self.collective == "reduce":
-                self.dist.reduce(self.stack, dst=0)  # the one collective of the group
-            else:
-                img = self.stack.view(self.frames, self.height, self.width, 3)
-                mine = self.rows[self.rank]
-                self.part[:n, :len(mine)] = img[:n, mine]
-                self.dist.gather(self.part, gather_list=self.parts, dst=0)  # the one collective of the group
-                if self.rank == 0:
-                    land = self.landing.transpose(0, 1).reshape(self.frames, self.world * self.most, self.width, 3)
-                    img[:n, self.dst_rows] = land[:n, self.src_rows]
+            img = self.stack.view(self.frames, self.height, self.width, 3)
+            img8 = self.stack8.view(self.frames, self.height, self.width, 3)
+            mine = self.rows[self.rank]
+            self.part[:n, :len(mine)] = img[:n, mine]
+            self.part8[:n, :len(mine)] = img8[:n, mine]
+            self.dist.gather(self.part, gather_list=self.parts, dst=0)  # the group's float rows
+            self.dist.gather(self.part8, gather_list=self.parts8, dst=0)  # and its 8-bit rows
             if self.rank == 0:
-                for f in range(n):
-                    self.r.finalize_u8_image(cfg, spp, self.images[f], self.images8[f])
+                land = self.landing.transpose(0, 1).reshape(self.frames, self.world * self.most, self.width, 3)
+                img[:n, self.dst_rows] = land[:n, self.src_rows]
+                land8 = self.landing8.transpose(0, 1).reshape(self.frames, self.world * self.most, self.width, 3)
+                img8[:n, self.dst_rows] = land8[:n, self.src_rows]
 
     def synchronize(self) -> None:
         self.r.synchronize()
