@@ -335,7 +335,7 @@ def main() -> int:
     # (+0.27 %, 3 of 3 rounds, profiles/r03/grid_share/). Not for the 0.4-4 s C4/C5 frames, whose tails are
     # a small part of them: there the 10 % left to the third frame sits idle (C4 -3.8 %)
     # Frames per launch (pt_render_frames, pathtracerwithcuda_amd.FrameGroup): each context renders G frames of
-    # the view in one pass launch (and, tiled, moves them with one collective), so the frames share one launch's
+    # the view in one pass launch (and, tiled, moves them with one gather per group), so the frames share one launch's
     # start and tail. Every frame is still rendered whole, with its own 8-bit output. Measured
     # (profiles/r04/group/), two contexts on the whole grid against one frame per launch on three (N = 1, 45 %
     # grids) or five (tiled, 25 %) contexts: the bench line at N = 1 13662-13697 Mrays/s with 8 frames per

@@ -151,8 +151,8 @@ class TiledFrame:
 
 
 class FrameGroup:
-    """`frames` frames per launch on this rank's bands (pt_render_frames), then ONE collective for all of
-    them: the group's float images are one [frames, height * width * 3] buffer, so the gather moves every
+    """`frames` frames per launch on this rank's bands (pt_render_frames), then one collective per group for all
+    of them: the group's float images are one [frames, height * width * 3] buffer, so the gather moves every
     frame's rows in one call (with a second for the ranks' own 8-bit rows; the reduce sums the whole stack and
     rank 0 writes the 8-bit images). The frames share one pass launch's start
     and tail instead of each paying its own, which is most of a small share's cost. Frame f
