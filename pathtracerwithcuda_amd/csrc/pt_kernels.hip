@@ -300,15 +300,20 @@ __device__ __forceinline__ unsigned int frame_local(unsigned int u, unsigned int
     return u;
 }
 
-// unit: the launch's unit (pass_rad index); lu: its unit within its frame copy (pt_render_frames; lu == unit for
-// one copy)
+// unit: the launch's unit (pass_rad index). frame_units: the units of one frame copy of a pt_render_frames launch
+// (0 for a launch of one frame); the unit within its frame copy is derived only where it is used (band costs, the
+// direct image path): the MULTI launches write pass_rad by the launch's unit, and the subtraction loop over the
+// frame copies, run for every finished path, cost up to G iterations per shading batch (round 5)
 __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfig& cfg, const DevOutput& out,
-                                            const PathState& ps, unsigned int unit, unsigned int lu, int first_pass,
-                                            int write_u8, int batch_log2, float clamp_hi, int depth) {
-    if (til.band_cost) atomicAdd(&til.band_cost[pixel_band(til, unit_to_pixel(til, lu >> batch_log2))], (unsigned int)depth);
+                                            const PathState& ps, unsigned int unit, unsigned int frame_units,
+                                            int first_pass, int write_u8, int batch_log2, float clamp_hi, int depth) {
+    if (til.band_cost) {
+        const unsigned int lu = frame_units ? frame_local(unit, frame_units) : unit;
+        atomicAdd(&til.band_cost[pixel_band(til, unit_to_pixel(til, lu >> batch_log2))], (unsigned int)depth);
+    }
     const v3 c = clamp3(ps.rad, 0.0f, clamp_hi);
     if (batch_log2 == 0 && !out.via_rad) {  // (never for several frame copies: they go through pass_rad)
-        const int pixel = unit_to_pixel(til, lu);
+        const int pixel = unit_to_pixel(til, unit);  // one frame copy here: the unit is its own frame's
         float* img = out.image + (size_t)pixel * 3;
         v3 sum;
         if (first_pass != 1) sum = mk3(img[0], img[1], img[2]) + c;
@@ -519,7 +524,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                     if (cfg.max_depth > 0) {
                         mode = LANE_NEW;
                     } else {
-                        finish_unit(til, cfg, out, ps, u, MULTI ? frame_local(u, frame_units) : u, first_pass,
+                        finish_unit(til, cfg, out, ps, u, MULTI ? frame_units : 0u, first_pass,
                                     write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
                     }
                 } else if (drained) {
@@ -558,7 +563,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                         if (cfg.max_depth > 0) {
                             mode = LANE_NEW;
                         } else {
-                            finish_unit(til, cfg, out, ps, unit, u, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
+                            finish_unit(til, cfg, out, ps, unit, 0u, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
                         }
                     }
                 } else if (drained) {
@@ -588,7 +593,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 if (cfg.max_depth > 0) {
                     mode = LANE_NEW;
                 } else {
-                    finish_unit(til, cfg, out, ps, unit, lu, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
+                    finish_unit(til, cfg, out, ps, unit, frame_units, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
                     mode = LANE_WANT;
                 }
             }
@@ -632,7 +637,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
 #else
                     const unsigned int un = unit;
 #endif
-                    finish_unit(til, cfg, out, ps, un, MULTI ? frame_local(un, frame_units) : un, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
+                    finish_unit(til, cfg, out, ps, un, MULTI ? frame_units : 0u, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
                     mode = LANE_WANT;
                 } else {
                     mode = LANE_NEW;  // its next segment starts in the next round's refill, with the new paths
