@@ -2,14 +2,13 @@
 """Benchmark of the radiance loop: Mrays/s and ms/frame at 1920x1080, 8 spp, 8 bounces on the
 Cornell + OBJ-mesh scene (BASELINE.json `metric`), on 1 GPU or tiled across N GPUs of one node.
 
-A step is one frame: 8 passes (batched into one persistent HIP launch plus an in-order accumulate)
-over the 1920x1080 frame and the 8-bit gamma output; with N > 1 each rank renders its interleaved 8-row bands and
-rank 0 gathers the ranks' rows of the float accumulation buffer with one RCCL gather (torch.distributed
-"nccl"; PT_FRAME_COLLECTIVE=reduce: one reduce of the whole buffer instead), after which rank 0
-writes the 8-bit image. Frames are queued with no host synchronisation on three renderer contexts
-(five when tiled), each launching on half (a quarter of) the grid, so one frame's tail overlaps the
-next frames' work (PT_BENCH_INFLIGHT=1:
-one at a time on the whole grid); the host-synchronised single-frame latency is reported beside it. Mrays/s = ray segments traced (the live-ray counts the
+A step is one frame: 8 passes over the 1920x1080 frame and its 8-bit gamma output. Frames are rendered in
+groups (pt_render_frames: G frames per persistent HIP launch, each through its own camera, plus one accumulate
+launch) on two renderer contexts, queued with no host synchronisation. With N > 1 each rank renders its
+interleaved 8-row bands of G = 8 N frames per launch and rank 0 gathers every rank's 8-bit rows with one RCCL
+gather per group (torch.distributed "nccl"; the float running sums stay on their ranks, as the reference's
+float image stays on the device, PT_FRAME_COLLECTIVE=gather moves them too, =reduce sums the float stack).
+The host-synchronised single-frame latency is reported beside it. Mrays/s = ray segments traced (the live-ray counts the
 reference's thread_shrink returns, summed over passes and depths and over ranks) / wall time.
 
     python bench.py [--gpus N --steps K --warmup W]   (defaults: 20 timed frames after 5, C4/C5 3 after 1)
@@ -372,8 +371,11 @@ def main() -> int:
         rs.append(q)
         if group > 1:
             # buffers for the most frames one launch of this run holds (the warm-up's or the timed run's)
+            # tiled, a group moves only its 8-bit rows to rank 0 ("gather8"): the frame the reference's application
+            # takes from the device each frame (Main/window.cpp:391); the float running sums stay on their ranks
             frames.append(pt.FrameGroup(q, width, height, max(1, min(group, max(args.steps, args.warmup))),
-                                        dist if distributed else None, BAND_ROWS, device=f"cuda:{local}"))
+                                        dist if distributed else None, BAND_ROWS, device=f"cuda:{local}",
+                                        collective=os.environ.get("PT_FRAME_COLLECTIVE", "gather8")))
         else:
             frames.append(pt.TiledFrame(q, width, height, dist if distributed else None, BAND_ROWS,
                                         device=f"cuda:{local}" if distributed else None))
@@ -445,6 +447,10 @@ def main() -> int:
     # compares them bitwise (float running sum and 8-bit image); the line carries config.image_matches_1gpu and a
     # mismatch exits 3
     matches_1gpu = None
+    if distributed and group > 1:
+        # "gather8": the float rows of the last timed launch's frames to rank 0 for the check (every rank)
+        frames[last_launch[0]].collect_float()
+        frames[last_launch[0]].synchronize()
     if distributed and rank == 0:
         ctx, cams = last_launch
         picks = sorted({0, len(cams) - 1})
@@ -631,7 +637,7 @@ def main() -> int:
     if distributed:
         line["config"]["image_matches_1gpu"] = matches_1gpu
         line["config"]["collective"] = {"backend": dist.get_backend(), "world_size": world,
-                                        "frame_collective": os.environ.get("PT_FRAME_COLLECTIVE", "gather")}
+                                        "frame_collective": frames[0].collective}
     if world == 1 and not args.no_cpu_baseline and args.workload in ("metric", "c1"):
         threads, why = host_threads(args.cpu_threads)
         line["cpu_baseline"] = cpu_baseline(wl, threads)

@@ -38,6 +38,9 @@ namespace pt {
 #ifndef PT_GEN_RING
 #define PT_GEN_RING 1
 #endif
+#ifndef PT_PARAM_RELOAD
+#define PT_PARAM_RELOAD 1
+#endif
 template <class T>
 __device__ __forceinline__ void opaque(T& x) {
     int* p = reinterpret_cast<int*>(&x);
@@ -438,7 +441,9 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     if (PROF) t_start = __builtin_amdgcn_s_memrealtime();
     while (true) {
         const LaunchParams* P = params;
+#if PT_PARAM_RELOAD
         asm volatile("" : "+s"(P));
+#endif
         P = uniform_ptr(P);
         DevScene sc = load_const(&P->sc);
         sc.materials = lds_mats;

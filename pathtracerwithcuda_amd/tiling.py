@@ -158,6 +158,12 @@ class FrameGroup:
     and tail instead of each paying its own, which is most of a small share's cost. Frame f
     of a launch is bit-identical to a TiledFrame's frame through the same camera.
 
+    "gather8" moves only the 8-bit rows per group: rank 0 ends with every frame's 8-bit image, the frame the
+    reference's application takes from the device each frame (Main/window.cpp:391 copies pixels_256_device
+    only; the float running sum stays on the device for the next passes), while each rank keeps the float
+    running sums of its own rows; collect_float() gathers those on demand. A quarter of the gather's bytes
+    (3 B per pixel, not 15).
+
     The renderer additionally needs render_frames and finalize_u8_image (the Renderer interface)."""
 
     def __init__(self, renderer, width: int, height: int, frames: int, dist=None, band_rows: int = 8,
@@ -171,7 +177,7 @@ class FrameGroup:
         self.rank = self.dist.get_rank() if self.dist else 0
         self.band_rows = band_rows
         self.collective = collective or os.environ.get("PT_FRAME_COLLECTIVE", "gather")
-        if self.collective not in ("gather", "reduce"):
+        if self.collective not in ("gather", "gather8", "reduce"):
             raise ValueError(f"unknown frame collective {self.collective!r}")
         device = device or "cuda:0"
         n = width * height * 3
@@ -214,8 +220,8 @@ class FrameGroup:
 
     def launch(self, cams, cfg, spp: int) -> None:
         """Queues passes 1..spp of len(cams) <= frames frames (frame f through cams[f]), then (world > 1) the
-        group's collective (gather: the float and the 8-bit rows of every rank; reduce: the float stack, then rank
-        0's 8-bit outputs), in order on the renderer's stream."""
+        group's collective (gather: the float and the 8-bit rows of every rank; gather8: the 8-bit rows; reduce: the
+        float stack, then rank 0's 8-bit outputs), in order on the renderer's stream."""
         n = len(cams)
         if not 1 <= n <= self.frames:
             raise ValueError(f"1..{self.frames} cameras per launch, got {n}")
@@ -238,18 +244,29 @@ class FrameGroup:
             self.r.render_frames(list(cams), cfg, self.images[:n], self.images8[:n], 1, spp, write_u8=2)
             if self.stream is None:
                 self.r.synchronize()
-            img = self.stack.view(self.frames, self.height, self.width, 3)
-            img8 = self.stack8.view(self.frames, self.height, self.width, 3)
-            mine = self.rows[self.rank]
-            self.part[:n, :len(mine)] = img[:n, mine]
-            self.part8[:n, :len(mine)] = img8[:n, mine]
-            self.dist.gather(self.part, gather_list=self.parts, dst=0)  # the group's float rows
-            self.dist.gather(self.part8, gather_list=self.parts8, dst=0)  # and its 8-bit rows
-            if self.rank == 0:
-                land = self.landing.transpose(0, 1).reshape(self.frames, self.world * self.most, self.width, 3)
-                img[:n, self.dst_rows] = land[:n, self.src_rows]
-                land8 = self.landing8.transpose(0, 1).reshape(self.frames, self.world * self.most, self.width, 3)
-                img8[:n, self.dst_rows] = land8[:n, self.src_rows]
+            if self.collective == "gather":
+                self._gather_rows(self.stack, self.part, self.parts, self.landing if self.rank == 0 else None, n)
+            self._gather_rows(self.stack8, self.part8, self.parts8, self.landing8 if self.rank == 0 else None, n)
+
+    def _gather_rows(self, stack, part, parts, landing, n: int) -> None:
+        """Frames 0..n-1 of `stack`: every rank's own rows to rank 0 (one gather of n frames' pieces; a launch of
+        fewer frames than the group moves only its own), placed there."""
+        img = stack.view(self.frames, self.height, self.width, 3)
+        mine = self.rows[self.rank]
+        part[:n, :len(mine)] = img[:n, mine]
+        self.dist.gather(part[:n], gather_list=[p[:n] for p in parts] if parts is not None else None, dst=0)
+        if landing is not None:
+            land = landing[:, :n].transpose(0, 1).reshape(n, self.world * self.most, self.width, 3)
+            img[:n, self.dst_rows] = land[:, self.src_rows]
+
+    def collect_float(self) -> None:
+        """"gather8": the float running sums of the last launch's frames, which stay on the ranks that rendered
+        their rows, gathered to rank 0 (a collective: every rank calls it). Queued on the renderer's stream; other
+        collectives need nothing."""
+        if not self.collect or self.collective != "gather8":
+            return
+        with self._on_stream():
+            self._gather_rows(self.stack, self.part, self.parts, self.landing if self.rank == 0 else None, self.last)
 
     def synchronize(self) -> None:
         self.r.synchronize()

@@ -58,6 +58,10 @@ def main() -> int:
         fr[i % inflight].launch(cams if group > 1 else cam, cfg, SPP)
     for f in fr:
         f.synchronize()
+    if group > 1 and collective == "gather8":  # the float rows stay on their ranks until asked for (every rank)
+        for f in fr:
+            f.collect_float()
+            f.synchronize()
     if rank == 0:
         for k, (r, f) in enumerate(zip(rs, fr)):
             if group > 1:

@@ -1,7 +1,8 @@
 """One rank of tests/test_gpu_multirank.py::test_rccl_one_rank_metric_frame: the production collective path on
 RCCL (torch.distributed "nccl") with a one-rank group on the one-GPU box, initialised exactly as bench.py
 initialises an N-GPU run (env:// rendezvous from torch.distributed.run, device_id given). The metric frame goes
-through a FrameGroup (three frames in one MULTI launch, one RCCL gather of the group) and a TiledFrame (one RCCL
+through a FrameGroup (three frames in one MULTI launch, one RCCL gather of the group), a "gather8" FrameGroup
+(two frames: their 8-bit rows with the launch, the float rows by collect_float) and a TiledFrame (one RCCL
 reduce of the float buffer); the images and the collective's facts are saved for the test to check.
 
     python -m torch.distributed.run --nproc-per-node 1 ... gpu_rccl_worker.py <out-prefix>
@@ -43,6 +44,22 @@ def main() -> int:
             img, img8 = g.download(f)
             np.save(f"{out}_group{f}_f.npy", img.reshape(-1, 3))
             np.save(f"{out}_group{f}_u8.npy", img8.reshape(-1, 3))
+    finally:
+        q.close()
+    q = pt.Renderer(local)
+    try:
+        # bench.py's tiled group: only the 8-bit rows move with the launch; the float rows on demand
+        q.upload(wl.scene, wl.cfg)
+        g = pt.FrameGroup(q, wl.width, wl.height, 3, dist, bench.BAND_ROWS, device=f"cuda:{local}",
+                          collective="gather8")
+        g.launch(cams[:2], wl.cfg, wl.spp)
+        g.synchronize()
+        img8s = [g.download(f)[1] for f in range(2)]
+        g.collect_float()
+        g.synchronize()
+        for f in range(2):
+            np.save(f"{out}_g8_{f}_f.npy", g.download(f)[0].reshape(-1, 3))
+            np.save(f"{out}_g8_{f}_u8.npy", img8s[f].reshape(-1, 3))
     finally:
         q.close()
     q = pt.Renderer(local)

@@ -50,7 +50,8 @@ def test_rccl_one_rank_metric_frame(require_gpu, tmp_path):
     """RCCL itself on the one-GPU box: torch.distributed "nccl" with a one-rank group, initialised as bench.py
     initialises its N-GPU runs (torch.distributed.run env:// rendezvous, device_id), carries the metric frame
     through the production collective path — a FrameGroup of three frames in one MULTI launch with one RCCL
-    gather, and a TiledFrame with one RCCL reduce — plus an all-reduce and a barrier. Every frame equals the
+    gather, the bench's "gather8" group (8-bit rows per launch, the float rows on demand), and a TiledFrame with
+    one RCCL reduce — plus an all-reduce and a barrier. Every frame equals the
     oracle's whole frame bit for bit, and librccl is the library the process loaded."""
     import bench
 
@@ -70,7 +71,7 @@ def test_rccl_one_rank_metric_frame(require_gpu, tmp_path):
     ref, ref8, _ = oracle.render(wl.scene.view, wl.cam, wl.cfg, 1, wl.spp)
     ref_t, ref8_t, _ = oracle.render(wl.scene.view, turned, wl.cfg, 1, wl.spp)
     for tag, (want, want8) in (("group0", (ref, ref8)), ("group1", (ref_t, ref8_t)), ("group2", (ref, ref8)),
-                               ("reduce", (ref, ref8))):
+                               ("reduce", (ref, ref8)), ("g8_0", (ref, ref8)), ("g8_1", (ref_t, ref8_t))):
         img = np.load(f"{out}_{tag}_f.npy")
         img8 = np.load(f"{out}_{tag}_u8.npy")
         assert np.array_equal(img.view(np.uint32), want.view(np.uint32)), f"{tag}: float image"
@@ -92,7 +93,8 @@ def test_bench_rccl_one_rank_self_check(require_gpu, tmp_path):
     assert line["config"]["frames_per_launch"] == 8 and line["config"]["orbit_rad_per_frame"] == 0.01, line["config"]
 
 
-@pytest.mark.parametrize("ranks,collective,inflight,group", [(2, "gather", 3, 4), (3, "reduce", 2, 3)])
+@pytest.mark.parametrize("ranks,collective,inflight,group", [(2, "gather", 3, 4), (3, "reduce", 2, 3),
+                                                            (3, "gather8", 2, 4)])
 def test_frame_groups_on_hip_equal_the_oracle(require_gpu, tmp_path, ranks, collective, inflight, group):
     """bench.py's PT_BENCH_GROUP path: FrameGroup contexts (pt_render_frames, one collective per group) with
     frames in flight; every frame of every context equals the oracle's frame of its camera."""

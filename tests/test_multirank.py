@@ -122,12 +122,21 @@ def _group_worker(rank, world, port, out_dir, collective):
         cfg, _ = _setup()
         cams = [pt.camera(W, H, yaw=y, pitch=0.08, radius=12.5, center=(0, 1.2, 0)) for y in CAM_YAWS]
         g = pt.FrameGroup(OracleFrameRenderer(scene), W, H, 3, dist, BAND, device="cpu", collective=collective)
+        def frames_of(n):
+            if collective != "gather8":
+                return [g.download(f) for f in range(n)]
+            # gather8: rank 0 has every frame's 8-bit image after the launch; the float rows follow on demand
+            img8 = [g.download(f)[1] for f in range(n)]
+            g.collect_float()
+            g.synchronize()
+            return [(g.download(f)[0], img8[f]) for f in range(n)]
+
         g.launch(cams, cfg, SPP)
         g.synchronize()
-        full = [g.download(f) for f in range(3)]
+        full = frames_of(3)
         g.launch(cams[1:], cfg, SPP)  # two frames: the stack's third frame is left as it was
         g.synchronize()
-        two = [g.download(f) for f in range(2)]
+        two = frames_of(2)
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), img=np.stack([a for a, _ in full]),
                  img8=np.stack([b for _, b in full]), img2=np.stack([a for a, _ in two]),
                  img82=np.stack([b for _, b in two]))
@@ -137,7 +146,7 @@ def _group_worker(rank, world, port, out_dir, collective):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world,collective", [(2, "gather"), (3, "gather"), (2, "reduce"), (1, "gather"),
-                                              (1, "reduce")])
+                                              (1, "reduce"), (2, "gather8"), (3, "gather8"), (1, "gather8")])
 def test_frame_group_equals_single_renders(tmp_path, world, collective):
     """World size 1 is bench.py --rccl's path: a one-rank group still takes the collective (band count 1, the
     gather's own piece placed, or the reduce of the one buffer)."""

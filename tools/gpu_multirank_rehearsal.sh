@@ -17,16 +17,17 @@ run() {  # name ranks port extra-env...
   cmp gpurun_out/$TAG/n1.png gpurun_out/$TAG/$m.png || exit 4
 }
 # b*: one frame per launch (PT_BENCH_GROUP=1); g*: the default frame groups at N > 1 (8 N frames per launch,
-# one collective per group): 5 steps = one launch of 5 frames
+# one collective per group; g4, g8, g4s20: the bench's default "gather8", the 8-bit rows per group and the
+# float rows after the timed run for the self-check): 5 steps = one launch of 5 frames
 run b2 2 29533 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=1
 run b3 3 29534 PT_FRAME_COLLECTIVE=reduce PT_BENCH_GROUP=1
 run b4 4 29535 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=1
 run b8 8 29536 PT_FRAME_COLLECTIVE=gather PT_BENCH_GROUP=1
 run g2 2 29537 PT_FRAME_COLLECTIVE=reduce
 run g3 3 29538 PT_FRAME_COLLECTIVE=gather
-run g4 4 29539 PT_FRAME_COLLECTIVE=gather
-run g8 8 29540 PT_FRAME_COLLECTIVE=gather
+run g4 4 29539 PT_BENCH_GROUP=0
+run g8 8 29540 PT_BENCH_GROUP=0
 # the driver's 20 steps: with G = 8 N frames per launch, one launch of 20 frames at N = 4 and 8
-S=20 run g4s20 4 29541 PT_FRAME_COLLECTIVE=gather
+S=20 run g4s20 4 29541 PT_BENCH_GROUP=0
 S=20 run g8s20 8 29542 PT_FRAME_COLLECTIVE=reduce
 echo "saved images identical to the 1-GPU image"
