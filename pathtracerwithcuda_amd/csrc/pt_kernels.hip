@@ -63,6 +63,29 @@ __device__ __forceinline__ T load_const(const T* p) {
 #endif
 }
 
+// PT_PARAM_LAZY (default 1): pass_kernel_u reads its configuration, tiling and output fields where it uses them
+// (const_ref) instead of copying the three structs at the top of every round. At 8 waves per SIMD a wave has
+// about 80 SGPRs, so the copies did not fit: every round reloaded ~30 dwords and spilled them into VGPR lanes
+// again (29 v_writelane and eight scalar-load waits per round, 4.8 M rounds per launch), and every use read them
+// back (v_readlane). Read at their uses they live for a few instructions: v_readlane 284 -> 59, v_writelane
+// 74 -> 46 in the bench kernel; metric 15411-15433 vs 15028-15144 Mrays/s (profiles/r05/lazy/ab.txt).
+// 0: the struct copies; 2: the configuration copied, the rest read at use.
+#ifndef PT_PARAM_LAZY
+#define PT_PARAM_LAZY 1
+#endif
+// A reference to *p whose loads go through the constant address space wherever they are used (the generic
+// pointer is an address-space cast of a constant one, which the compiler's address-space inference sees
+// through once everything is inlined): the fields are read at their uses, not copied at one point.
+template <class T>
+__device__ __forceinline__ const T& const_ref(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(4))) const T ConstT;
+    return *(const T*)(const ConstT*)(unsigned long long)p;
+#else
+    return *p;
+#endif
+}
+
 // MINW = minimum waves per SIMD requested from the register allocator; the persistent loop is
 // latency-bound, so occupancy is the first-order knob.
 //
@@ -448,9 +471,19 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         DevScene sc = load_const(&P->sc);
         sc.materials = lds_mats;
         sc.spheres = lds_spheres;
+#if PT_PARAM_LAZY
+#if PT_PARAM_LAZY == 2
+        const DevConfig cfg = load_const(&P->cfg);
+#else
+        const DevConfig& cfg = const_ref(&P->cfg);
+#endif
+        const DevTiling& til = const_ref(&P->til);
+        const DevOutput& out = const_ref(&P->out);
+#else
         const DevConfig cfg = load_const(&P->cfg);
         const DevTiling til = load_const(&P->til);
         const DevOutput out = load_const(&P->out);
+#endif
         const bool roots = sc.mesh_num <= PT_ROOT_MESHES;  // wave-uniform
         if (PROF) {
             prof[0]++;
@@ -466,7 +499,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             // lanes take generated paths from the ring in lane order; when it runs dry the wave fetches the next
             // chunk and generates all of it (gen_ring_fill below), then the remaining lanes take from the new ring
             const int taken = __popcll(need_mask);
-            const int rank = __popcll(need_mask & lanes_below(lane));
+            const int rank = count_below(need_mask);
             const int avail = ring_end - ring_head;
             bool got = false;
             unsigned int u = ~0u;

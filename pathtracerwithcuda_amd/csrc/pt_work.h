@@ -23,6 +23,10 @@ namespace pt {
 __device__ __forceinline__ unsigned long long lanes_below(int lane) {
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
+// popcount(m & lanes_below(lane)) of the calling lane: two v_mbcnt, no 64-bit mask held in registers
+__device__ __forceinline__ int count_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned int)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned int)m, 0u));
+}
 
 // Unit u of this launch's share of the frame -> pixel index (DevTiling: bands of band_rows rows
 // dealt round-robin over band_count owners).
