@@ -86,6 +86,20 @@ __device__ __forceinline__ const T& const_ref(const T* p) {
 #endif
 }
 
+// PT_LANE_NOW (default 1): pass_kernel_u recomputes its lane index where it uses it (two v_mbcnt in a volatile asm,
+// which the compiler neither merges nor hoists) and keeps its wave index in an SGPR, instead of holding
+// threadIdx-derived values in VGPRs across the loop: at 64 VGPRs they were spilled to scratch and reloaded, with a
+// wait on memory, in the refill and at every path's end. No instance spills to scratch now (the bench kernel had
+// 16 B, C5's 12 B); metric 15628-15659 vs 15222-15411 Mrays/s (profiles/r05/lane/ab.txt).
+#ifndef PT_LANE_NOW
+#define PT_LANE_NOW 1
+#endif
+__device__ __forceinline__ int lane_now() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 // MINW = minimum waves per SIMD requested from the register allocator; the persistent loop is
 // latency-bound, so occupancy is the first-order knob.
 //
@@ -387,7 +401,17 @@ template <int MINW, bool PROF, int FEAT, bool MULTI = false>
 __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
                                                                 int walk_steps, int tri_min, int walk_min) {
+#if PT_LANE_NOW
+    // the wave's index in the workgroup, wave-uniform (an SGPR); the lane index is recomputed at each use
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#define PT_LANE lane_now()
+#define PT_TID (wave * 64 + lane_now())
+#else
+    const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
+#define PT_LANE lane
+#define PT_TID threadIdx.x
+#endif
     const LaunchParams* P0 = params;
     // workgroup copies in LDS: the first mesh ranges, every material and every sphere (the launch
     // reserves their bytes of dynamic LDS; pass_kernel_u runs only when that fits, PT_LDS_TABLES)
@@ -396,7 +420,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     __shared__ float4 lds_root[2 * PT_ROOT_MESHES];
 #if PT_GEN_RING
     __shared__ float4 lds_ring[PT_UBLOCK / 64][2 * PT_RING];  // one generation ring per wave
-    float4* ring = lds_ring[threadIdx.x >> 6];
+    float4* ring = lds_ring[wave];
     int ring_head = 0, ring_end = 0;  // wave-uniform: entries [ring_head, ring_end) are generated, not yet taken
     // the lane's (pixel, pass) unit lives in LDS: it is read once, at the path's end (finish_unit), and held in a
     // VGPR it was spilled to scratch around the ring fill (written back after every shading batch: 0.6 GB of
@@ -514,8 +538,8 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 if (PROF) { prof[7] += (unsigned long long)n; gen_batches++; }
                 // gen_ring_fill: lane i generates unit cursor.cur + i. The camera is read through the scalar cache,
                 // so a chunk that spans frames (MULTI) is generated one frame at a time
-                if (lane < n) {
-                    const unsigned int gu = cursor.cur + (unsigned int)lane;
+                if (PT_LANE < n) {
+                    const unsigned int gu = cursor.cur + (unsigned int)PT_LANE;
                     // the chunk's frames f_lo..f_hi are wave-uniform (scalar arithmetic on the chunk's bounds): one
                     // pass per frame, each lane generating in its own frame's pass (one pass unless the chunk spans
                     // frames)
@@ -537,7 +561,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                                 opaque(p2);
                             }
                             generate_path(cam, cfg, pixel, hseed, &g);
-                            gen_ring_put(ring, lane, g, path_seed(hseed, pixel), gu);
+                            gen_ring_put(ring, PT_LANE, g, path_seed(hseed, pixel), gu);
                         }
                     }
                 }
@@ -557,7 +581,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (PROF && drained && t_drain == 0) t_drain = __builtin_amdgcn_s_memrealtime();
             if (want) {
                 if (got) {
-                    lds_unit[threadIdx.x] = u;
+                    lds_unit[PT_TID] = u;
                     depth = 0;
                     if (cfg.max_depth > 0) {
                         mode = LANE_NEW;
@@ -573,7 +597,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
 #else
         if (need_mask) {
             const unsigned int u = work_take(out.fetch, regions.stride, regions, (unsigned int)chunk, need_mask, want,
-                                             lanes_below(lane), cursor, drained);
+                                             lanes_below(PT_LANE), cursor, drained);
             if (PROF) {
                 const unsigned long long started = __ballot(want && u != ~0u);
                 prof[7] += (unsigned long long)__popcll(started);
@@ -671,7 +695,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 depth++;
                 if (!alive || depth >= cfg.max_depth) {
 #if PT_GEN_RING
-                    const unsigned int un = lds_unit[threadIdx.x];
+                    const unsigned int un = lds_unit[PT_TID];
 #else
                     const unsigned int un = unit;
 #endif
@@ -763,7 +787,7 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         if (PROF) prof[10] += __builtin_readcyclecounter() - tc;
     }
 
-    if (lane == 0) {
+    if (PT_LANE == 0) {
         atomicAdd(&P0->out.stats[0], segments);
         if (PROF) {
 #pragma unroll
@@ -780,6 +804,8 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             atomicAdd(&tl[10], gen_batches); atomicAdd(&tl[11], live_lane_rounds);
         }
     }
+#undef PT_LANE
+#undef PT_TID
 }
 
 // The running sum over a batch of passes, in pass order (path_tracer_kernel.cu:644-651 applied
