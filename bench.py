@@ -7,7 +7,10 @@ groups (pt_render_frames: G frames per persistent HIP launch, each through its o
 launch) on two renderer contexts, queued with no host synchronisation. With N > 1 each rank renders its
 interleaved 8-row bands of G = 8 N frames per launch and rank 0 gathers every rank's 8-bit rows with one RCCL
 gather per group (torch.distributed "nccl"; the float running sums stay on their ranks, as the reference's
-float image stays on the device, PT_FRAME_COLLECTIVE=gather moves them too, =reduce sums the float stack).
+float image stays on the device; --collective gather moves them too, --collective reduce sums the float stack on
+rank 0, the north star's RCCL reduce). Each rank of a multi-GPU run works under a stage watchdog and a collective
+timeout (--stage-timeout, 180 s): a rank stuck in a stage exits 124 with a stderr line naming it and the stage, and
+the line reports every rank's render and collective time per launch (config.per_rank).
 The host-synchronised single-frame latency is reported beside it. Mrays/s = ray segments traced (the live-ray counts the
 reference's thread_shrink returns, summed over passes and depths and over ranks) / wall time.
 
@@ -33,6 +36,7 @@ KNOT = (350, 100)  # 70,000 triangles: the ~70k-triangle bunny stand-in (SURVEY.
 CAMERA = dict(pitch=0.08, radius=12.5, center=(0.0, 1.2, 0.0))
 BAND_ROWS = int(os.environ.get("PT_BAND_ROWS", "8"))  # rows per interleaved band of the tiled frame
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_MEASURED_GBS = 6290.0  # MI355X_MICROARCH.md:36: 6.29 TB/s measured (float4 copy), "≈6.3 TB/s achievable" (:296)
 SIMDS = 256 * 4  # 256 CUs x 4 SIMDs
 CLOCK_HZ = 2.4e9  # MI355X_MICROARCH.md: max clock 2400 MHz
 
@@ -240,6 +244,50 @@ def load_profile(workload: str) -> dict:
         return {}
 
 
+def init_distributed(dist, backend: str, world: int, local: int, timeout_s: float, device=None) -> None:
+    """The process group of a multi-GPU run (SURVEY.md §8(e)): env:// rendezvous from torch.distributed.run, or a
+    one-rank in-process group (bench.py --rccl run directly), with a collective timeout, so that a collective whose
+    peer never arrives raises instead of waiting forever ("nccl" is RCCL on ROCm; device_id binds the communicator
+    to this rank's GPU). The StageWatch beside it ends a rank that is stuck anywhere else."""
+    import datetime
+
+    # the collective timeout outlasts the stage limit, so the StageWatch names the stuck stage first
+    kw = {"timeout": datetime.timedelta(seconds=max(1.0, float(timeout_s) + 60.0))}
+    if backend == "nccl" and device is not None:
+        kw["device_id"] = device
+    if world == 1 and "MASTER_ADDR" not in os.environ:
+        dist.init_process_group(backend, store=dist.HashStore(), rank=0, world_size=1, **kw)
+    else:
+        dist.init_process_group(backend, **kw)
+
+
+def rank_breakdown(dist, frames, world: int, device) -> dict:
+    """Per rank, the timed run's mean render and collective time per launch (StageClock: HIP events on the renderer
+    streams, launch start -> passes rendered -> collective done), gathered to every rank: where a slow multi-GPU
+    point spends its time. Every rank calls it (a collective)."""
+    import torch
+
+    t = [x for f in frames for x in f.clock.timings()]
+    n = len(t)
+    mine = [sum(a for a, _ in t) / max(n, 1), sum(b for _, b in t) / max(n, 1),
+            max((a for a, _ in t), default=0.0), max((b for _, b in t), default=0.0), float(n)]
+    x = torch.tensor(mine, dtype=torch.float64, device=device)
+    parts = [torch.zeros_like(x) for _ in range(world)]
+    dist.all_gather(parts, x)
+    rows = [q.tolist() for q in parts]
+    return {
+        "render_ms_per_launch": [round(r[0], 4) for r in rows],
+        "collective_ms_per_launch": [round(r[1], 4) for r in rows],
+        "render_ms_per_launch_max_over_ranks": round(max(r[0] for r in rows), 4),
+        "collective_ms_per_launch_max_over_ranks": round(max(r[1] for r in rows), 4),
+        "render_ms_slowest_launch": round(max(r[2] for r in rows), 4),
+        "collective_ms_slowest_launch": round(max(r[3] for r in rows), 4),
+        "launches_timed_per_rank": [int(r[4]) for r in rows],
+        "source": "HIP events on each rank's renderer streams: launch start -> passes rendered -> collective done "
+                  "(frames in flight overlap, so a launch's render time includes waiting for the GPU)",
+    }
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -261,6 +309,15 @@ def main() -> int:
     ap.add_argument("--orbit", type=float, default=0.0, metavar="RAD",
                     help="advance the camera's yaw by RAD per frame (an interactive caller's moving camera); every "
                          "frame then has its own camera, 0 (default) keeps one camera for all frames")
+    ap.add_argument("--collective", choices=["gather8", "gather", "reduce"], default=None,
+                    help="the frame collective of a multi-GPU run (default: PT_FRAME_COLLECTIVE, else gather8 with frame "
+                         "groups): gather8 moves each rank's 8-bit rows to rank 0 (the float running sums stay on their "
+                         "ranks), gather moves the float rows too, reduce sums the float buffers on rank 0 (north_star's "
+                         "RCCL reduce of the accumulation buffer)")
+    ap.add_argument("--stage-timeout", type=float, default=float(os.environ.get("PT_BENCH_STAGE_TIMEOUT", "180")),
+                    help="multi-GPU runs: seconds a rank may spend in one stage (init, upload, warm-up, timed run, "
+                         "collectives, self-check) before it exits with 124 and a stderr line naming the rank and the "
+                         "stage; also the collective timeout of the process group")
     ap.add_argument("--rccl", action="store_true",
                     help="at N = 1: run the multi-GPU path anyway, through a one-rank RCCL (torch 'nccl') group: "
                          "bands = 1, the frame's gather / reduce, barrier and all-reduce on RCCL, and the "
@@ -312,18 +369,13 @@ def main() -> int:
         local = 0
     # the multi-GPU code path: every N > 1 run, and N = 1 with --rccl (a one-rank group in this process)
     distributed = world > 1 or args.rccl
+    # fail-fast: every stage of a multi-GPU rank runs under a watchdog (pt.StageWatch), and collectives time out
+    watch = pt.StageWatch(rank, args.stage_timeout if distributed else 0.0)
     if distributed:
+        watch.stage("init process group")
         torch.cuda.set_device(local)
-        if world == 1 and "MASTER_ADDR" not in os.environ:  # --rccl run directly: a one-rank group in-process
-            store = dist.HashStore()
-            if backend == "nccl":
-                dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda", local))
-            else:
-                dist.init_process_group(backend, store=store, rank=0, world_size=1)
-        elif backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        init_distributed(dist, backend, world, local, args.stage_timeout, torch.device("cuda", local))
+        watch.stage("scene and upload")
     # frames in flight: one renderer context (own stream, image and pass buffers) per frame in flight,
     # so the next frame's workgroups fill the previous frame's tail; 1 = one at a time.
     # Each launch takes 1 / (F - 1) of the occupancy-sized grid (pt_set_grid_share). Measured best
@@ -356,6 +408,9 @@ def main() -> int:
         1 if heavy or args.workload == "c1" or wl.spp > 8 else 8 * world)
     inflight = int(os.environ.get("PT_BENCH_INFLIGHT", "0")) or (
         2 if group > 1 else 3 if world == 1 else 5)
+    collective = args.collective or os.environ.get("PT_FRAME_COLLECTIVE") or ("gather8" if group > 1 else "gather")
+    if group == 1 and collective == "gather8":
+        collective = "gather"  # one frame per launch: rank 0 gathers the float rows and writes the 8-bit image
     grid_share = int(os.environ.get("PT_BENCH_GRID_SHARE", "0")) or (
         (45 if inflight == 3 and not heavy and group == 1 else 100 // (inflight - 1)) if inflight >= 3 else 100)
     scene, cfg, cam = wl.scene, wl.cfg, wl.cam
@@ -375,14 +430,15 @@ def main() -> int:
             # takes from the device each frame (Main/window.cpp:391); the float running sums stay on their ranks
             frames.append(pt.FrameGroup(q, width, height, max(1, min(group, max(args.steps, args.warmup))),
                                         dist if distributed else None, BAND_ROWS, device=f"cuda:{local}",
-                                        collective=os.environ.get("PT_FRAME_COLLECTIVE", "gather8")))
+                                        collective=collective))
         else:
             frames.append(pt.TiledFrame(q, width, height, dist if distributed else None, BAND_ROWS,
-                                        device=f"cuda:{local}" if distributed else None))
+                                        device=f"cuda:{local}" if distributed else None, collective=collective))
     r = rs[0]
     schedule = r.schedule()
 
     # roofline inputs: one instrumented (untimed) frame for the visit counts
+    watch.stage("instrumented frame")
     r.set_instrumented(True)
     r.stats_reset()
     r.render(cam, cfg, 1, spp, write_u8=0)
@@ -427,19 +483,29 @@ def main() -> int:
             nframe += 1
             frame_no += n
 
+    watch.stage("warm-up")
     run(args.warmup)
     torch.cuda.synchronize()
     for q in rs:
         q.stats_reset()
+    for f in frames:
+        f.clock.reset()
     if distributed:
+        watch.stage("barrier before the timed run")
         dist.barrier()
     torch.cuda.synchronize()
+    watch.stage("timed run")
     t0 = time.perf_counter()
     run(args.steps)
     torch.cuda.synchronize()
     if distributed:
+        watch.stage("barrier after the timed run")
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    breakdown = None
+    if distributed:
+        watch.stage("per-rank breakdown")
+        breakdown = rank_breakdown(dist, frames, world, torch.device("cuda", local))
 
     # The distributed path must produce the 1-GPU frame. Outside the timed region, rank 0 takes the last TIMED
     # launch's first and last frame (with frame groups: the MULTI kernel's frames, as every timed frame is made)
@@ -447,6 +513,7 @@ def main() -> int:
     # compares them bitwise (float running sum and 8-bit image); the line carries config.image_matches_1gpu and a
     # mismatch exits 3
     matches_1gpu = None
+    watch.stage("self-check")
     if distributed and group > 1:
         # "gather8": the float rows of the last timed launch's frames to rank 0 for the check (every rank)
         frames[last_launch[0]].collect_float()
@@ -478,6 +545,7 @@ def main() -> int:
     # single-frame latency (one frame at a time, host-synchronised), reported beside the throughput; the
     # dominant kernel's launch duration for the roofline is taken here too, with no other frame in flight
     # (with frames in flight the HIP events of one launch also span the overlapping launch's work)
+    watch.stage("single-frame latency")
     lat_frames = max(3, min(5, args.steps))
     r.set_grid_share(100)
     r.stats_reset()
@@ -492,6 +560,7 @@ def main() -> int:
     solo_ms, solo_launches = r.kernel_time_kind(kind)
 
     if distributed:
+        watch.stage("max over ranks")
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -504,8 +573,11 @@ def main() -> int:
 
     if rank != 0:
         if distributed:
+            watch.stage("destroy process group")
             dist.destroy_process_group()
+        watch.close()
         return 0
+    watch.stage("report")
 
     if args.save_image:  # the last timed launch's first frame (the frame the self-check compares)
         from pathtracerwithcuda_amd.imageio import write_png
@@ -571,7 +643,11 @@ def main() -> int:
         hbm_gbs = traffic / avg_launch_s / 1e9
         hbm = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": round(traffic),
+               "frac_of_measured": round(hbm_gbs / HBM_MEASURED_GBS, 4), "measured_peak": HBM_MEASURED_GBS,
                "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (gfx950 FETCH x2), profiles/traffic.json"}
+    valu = {"achieved": round(valu_achieved, 1) if valu_achieved else None, "peak": valu_peak,
+            "unit": "G VALU wave-instructions/s",
+            "frac": round(valu_achieved / valu_peak, 4) if valu_achieved else None}
     line = {
         "metric": "Mrays/sec + ms/frame @1920x1080, 8spp, 8-bounce; 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -605,12 +681,10 @@ def main() -> int:
         },
         "roofline": {
             "bound": "valu",
-            "achieved": round(valu_achieved, 1) if valu_achieved else None,
-            "peak": valu_peak,
-            "unit": "G VALU wave-instructions/s",
-            "frac": round(valu_achieved / valu_peak, 4) if valu_achieved else None,
+            **{k: valu[k] for k in ("achieved", "peak", "unit", "frac")},
             "traffic": round(traffic) if traffic is not None else None,
             "hbm": hbm,
+            "valu": valu,
             "valu_insts_per_launch": round(valu_insts) if valu_insts else None,
             "frac_rocprof_avg": round(valu_rocprof / valu_peak, 4) if valu_rocprof else None,
             "rocprof_avg_launch_ms": rp_ms if valu_rocprof else None,
@@ -634,10 +708,16 @@ def main() -> int:
         },
         "cpu_baseline": None,
     }
+    # The roofline that binds is whichever resource the kernel is closer to: VALU issue (the metric frame, C2, C3, C5)
+    # or HBM (C4's 51-MB tree: 0.61 of HBM against 0.51 of VALU, profiles/r05/workloads/); the other stays beside it
+    rf = line["roofline"]
+    if hbm is not None and (valu["frac"] is None or hbm["frac"] > valu["frac"]):
+        rf.update(bound="hbm", achieved=hbm["achieved"], peak=hbm["peak"], unit=hbm["unit"], frac=hbm["frac"])
     if distributed:
         line["config"]["image_matches_1gpu"] = matches_1gpu
         line["config"]["collective"] = {"backend": dist.get_backend(), "world_size": world,
                                         "frame_collective": frames[0].collective}
+        line["config"]["per_rank"] = breakdown
     if world == 1 and not args.no_cpu_baseline and args.workload in ("metric", "c1"):
         threads, why = host_threads(args.cpu_threads)
         line["cpu_baseline"] = cpu_baseline(wl, threads)
@@ -645,10 +725,12 @@ def main() -> int:
         line["cpu_baseline"]["threads_from"] = why
     print(json.dumps(line), file=result_out, flush=True)
     if distributed:
+        watch.stage("destroy process group")
         dist.destroy_process_group()
-        if not matches_1gpu:
-            print("[bench] the tiled frame differs from the 1-GPU frame", file=sys.stderr)
-            return 3
+    watch.close()
+    if distributed and not matches_1gpu:
+        print("[bench] the tiled frame differs from the 1-GPU frame", file=sys.stderr)
+        return 3
     return 0
 
 

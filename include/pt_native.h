@@ -96,7 +96,8 @@ int pt_render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_conf
  * bit-identical to pt_render_passes(cams[f]) on images[f]; the context's tiling applies to every frame.
  * With the single-kernel schedule one launch per batch of passes renders all the frames, so they share
  * one launch's start-up and tail; otherwise they render one after another. Asynchronous.
- * PT_E_ARG when the share's units times `frames` exceed 2^30 (one launch's 32-bit unit numbering). */
+ * PT_E_ARG when the share's units times `frames` exceed 2^30 (one launch's 32-bit unit numbering), or when
+ * two frames share a buffer (every frame's running sum is accumulated at the same time). */
 int pt_render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, const pt_configuration* config,
                      int first_pass, int pass_count, int write_u8, float* const* images,
                      unsigned char* const* images256);

@@ -13,8 +13,9 @@ import sys
 from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-CSRC = os.path.join(HERE, "csrc")
-# PT_LIBDIR / PT_EXTRA_FLAGS: an alternative build (compiler-flag A/B runs); the product is lib/
+# PT_CSRC / PT_LIBDIR / PT_EXTRA_FLAGS: an alternative build (a patched source copy, compiler-flag A/B runs,
+# tools/build_dup.sh); the product is csrc/ built into lib/
+CSRC = os.environ.get("PT_CSRC") or os.path.join(HERE, "csrc")
 LIBDIR = os.environ.get("PT_LIBDIR") or os.path.join(HERE, "lib")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(LIBDIR, "libpt_hip.so")

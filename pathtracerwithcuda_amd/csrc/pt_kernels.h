@@ -43,8 +43,11 @@ hipError_t launch_accumulate(const LaunchParams* params_dev, int units, int firs
 // every frame of a pt_render_frames launch at once; ptrs_dev: {images[0..frames), images256[0..frames)} on the device
 hipError_t launch_accumulate_frames(const LaunchParams* params_dev, int units, int first_pass, int batch_log2,
                                     int write_u8, int frames, const uint64_t* ptrs_dev, hipStream_t stream);
+// src: the running sum the pass is added to (null: P->out.image in place)
 hipError_t launch_accumulate_one(const LaunchParams* params_dev, int unit_begin, int unit_end, int pass, int batch_log2,
-                                 int j, int write_u8, const float* rad, hipStream_t stream);
+                                 int j, int write_u8, const float* rad, const float* src, hipStream_t stream);
+// order-independent digest of the 32-bit words [begin, end) of p, added into *out (device)
+hipError_t launch_digest_words(const void* p, size_t begin, size_t end, unsigned long long* out, hipStream_t stream);
 hipError_t launch_extend(const LaunchParams* P, bool gen, bool leaf1, bool stats, int depth, int pass, hipStream_t s);
 hipError_t launch_shade(const LaunchParams* P, bool first, bool last, bool stats, int depth, int pass, hipStream_t s);
 int shade_grid_waves();

@@ -21,33 +21,9 @@
 
 namespace pt {
 
-// PT_DUP (diagnostic builds only, -DPT_DUP=n via PT_EXTRA_FLAGS into a separate PT_LIBDIR): run one
-// phase twice on opaque copies of its inputs and discard the copy's result, so that the PMC
-// difference SQ_INSTS_VALU(dup) - SQ_INSTS_VALU(normal) is the VALU count of that phase over the
-// same dynamic paths (1 shading, 2 box stage, 3 triangle stage, 4 path generation). The product
-// build has PT_DUP 0 and none of this code.
-#ifndef PT_DUP
-#define PT_DUP 0
-#endif
-#ifndef PT_PROF_MESH
-#define PT_PROF_MESH 0
-#endif
-// PT_GEN_RING (default 1): pass_kernel_u generates camera paths a whole chunk at a time, by the full wave, into a
-// per-wave LDS ring that refills pop from (gen_ring_fill / gen_ring_take). 0: each refill generates its own
-// lanes' paths (round 4's refill: 9.2 lanes per generation instruction on the metric frame).
-#ifndef PT_GEN_RING
-#define PT_GEN_RING 1
-#endif
-#ifndef PT_PARAM_RELOAD
-#define PT_PARAM_RELOAD 1
-#endif
-template <class T>
-__device__ __forceinline__ void opaque(T& x) {
-    int* p = reinterpret_cast<int*>(&x);
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 4); i++) asm volatile("" : "+v"(p[i]));
-}
-
+// One path per feature: the measured alternatives of rounds 4-5 (refill-time path generation, struct copies of the
+// launch parameters, threadIdx-held lane indices) and the diagnostic phase duplicates (tools/build_dup.sh) live as
+// patches under profiles/ (profiles/r06/pruned/), not as preprocessor arms here.
 
 // A copy of *p read through the constant address space: the loads are known not to alias the
 // kernel's stores, so a wave-uniform p becomes scalar loads into SGPRs (s_load_dwordx*), not
@@ -63,16 +39,12 @@ __device__ __forceinline__ T load_const(const T* p) {
 #endif
 }
 
-// PT_PARAM_LAZY (default 1): pass_kernel_u reads its configuration, tiling and output fields where it uses them
-// (const_ref) instead of copying the three structs at the top of every round. At 8 waves per SIMD a wave has
-// about 80 SGPRs, so the copies did not fit: every round reloaded ~30 dwords and spilled them into VGPR lanes
-// again (29 v_writelane and eight scalar-load waits per round, 4.8 M rounds per launch), and every use read them
-// back (v_readlane). Read at their uses they live for a few instructions: v_readlane 284 -> 59, v_writelane
-// 74 -> 46 in the bench kernel; metric 15411-15433 vs 15028-15144 Mrays/s (profiles/r05/lazy/ab.txt).
-// 0: the struct copies; 2: the configuration copied, the rest read at use.
-#ifndef PT_PARAM_LAZY
-#define PT_PARAM_LAZY 1
-#endif
+// pass_kernel_u reads its configuration, tiling and output fields where it uses them (const_ref) instead of copying
+// the three structs at the top of every round. At 8 waves per SIMD a wave has about 80 SGPRs, so the copies did not
+// fit: every round reloaded ~30 dwords and spilled them into VGPR lanes again (29 v_writelane and eight scalar-load
+// waits per round, 4.8 M rounds per launch), and every use read them back (v_readlane). Read at their uses they live
+// for a few instructions: v_readlane 284 -> 59, v_writelane 74 -> 46 in the bench kernel; metric 15411-15433 vs
+// 15028-15144 Mrays/s (profiles/r05/lazy/ab.txt).
 // A reference to *p whose loads go through the constant address space wherever they are used (the generic
 // pointer is an address-space cast of a constant one, which the compiler's address-space inference sees
 // through once everything is inlined): the fields are read at their uses, not copied at one point.
@@ -86,14 +58,11 @@ __device__ __forceinline__ const T& const_ref(const T* p) {
 #endif
 }
 
-// PT_LANE_NOW (default 1): pass_kernel_u recomputes its lane index where it uses it (two v_mbcnt in a volatile asm,
-// which the compiler neither merges nor hoists) and keeps its wave index in an SGPR, instead of holding
-// threadIdx-derived values in VGPRs across the loop: at 64 VGPRs they were spilled to scratch and reloaded, with a
-// wait on memory, in the refill and at every path's end. No instance spills to scratch now (the bench kernel had
-// 16 B, C5's 12 B); metric 15628-15659 vs 15222-15411 Mrays/s (profiles/r05/lane/ab.txt).
-#ifndef PT_LANE_NOW
-#define PT_LANE_NOW 1
-#endif
+// pass_kernel_u recomputes its lane index where it uses it (two v_mbcnt in a volatile asm, which the compiler neither
+// merges nor hoists) and keeps its wave index in an SGPR, instead of holding threadIdx-derived values in VGPRs across
+// the loop: at 64 VGPRs they were spilled to scratch and reloaded, with a wait on memory, in the refill and at every
+// path's end. No instance spills to scratch now (the bench kernel had 16 B, C5's 12 B); metric 15628-15659 vs
+// 15222-15411 Mrays/s (profiles/r05/lane/ab.txt).
 __device__ __forceinline__ int lane_now() {
     int l;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
@@ -227,8 +196,7 @@ __global__ __launch_bounds__(PT_BLOCK, MINW) void pass_kernel(const LaunchParams
 // (+2.5 % over starting survivors inside the shading batch, profiles/r02/onesite.txt). Every lane
 // still computes exactly the reference sequence for its path (same node order, same tests, same draws
 // keyed by (pass, pixel, depth)); only the interleaving between lanes changes.
-// GEN: holding a unit whose camera path is not generated yet (a refill generates one frame's paths)
-enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3, LANE_TRI = 4, LANE_NEW = 5, LANE_GEN = 6 };
+enum : int { LANE_WANT = 0, LANE_WALK = 1, LANE_READY = 2, LANE_DONE = 3, LANE_TRI = 4, LANE_NEW = 5 };
 
 // Starts the walk of the first mesh at or after `mesh` with a non-empty node range. The ranges of the
 // first PT_LDS_MESHES meshes come from the workgroup's LDS copy (lds_mesh, filled at kernel start), the
@@ -366,10 +334,10 @@ __device__ __forceinline__ void finish_unit(const DevTiling& til, const DevConfi
     }
 }
 
-// ---- the generation ring (PT_GEN_RING) ---------------------------------------------------------------------
+// ---- the generation ring --------------------------------------------------------------------------------------
 // generate_ray_kernel (:299-379) runs once per new path. Generated where a refill hands out units, it executes
-// with only the refilled lanes active: 9.2 of 64 on the metric frame, 7 % of the kernel's VALU (round 4's PT_DUP
-// split). Here a wave that runs out of generated paths fetches its next chunk of units (one returning atomic, as
+// with only the refilled lanes active: 9.2 of 64 on the metric frame, 7 % of the kernel's VALU (round 4's phase
+// split, tools/build_dup.sh). Here a wave that runs out of generated paths fetches its next chunk of units (one returning atomic, as
 // before) and ALL its lanes generate the chunk's camera paths at once, lane i unit i, into the wave's 64-entry
 // ring in LDS; refills then pop entries in lane order. An entry is 32 B: {origin, path seed} {direction, unit}.
 // The other per-path fields are constants at generation (throughput 1, radiance 0, air, depth 0). Every path is
@@ -395,30 +363,22 @@ __device__ __forceinline__ void gen_ring_get(const float4* ring, int e, PathStat
 // batches, lanes in triangle batches, lanes refilled, then cycles and the drained/ready/idle counts,
 // and the launch timeline in stats[32..41].
 // FEAT: the scene features shade_hit can reach (pt_path.h PT_FEAT_*).
-// MULTI: the pt_render_frames instance (several frames per launch, LANE_GEN refills); the single-frame
-// instances keep the refill without that state (2 % faster on the bench frame, profiles/r04/group/)
+// MULTI: the pt_render_frames instance (several frames per launch: a ring fill that spans frames generates them one
+// frame at a time); the single-frame instances go without that loop
 template <int MINW, bool PROF, int FEAT, bool MULTI = false>
 __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchParams* __restrict__ params, int first_pass,
                                                                 int write_u8, int chunk, int batch_log2, int shade_min,
                                                                 int walk_steps, int tri_min, int walk_min) {
-#if PT_LANE_NOW
     // the wave's index in the workgroup, wave-uniform (an SGPR); the lane index is recomputed at each use
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 #define PT_LANE lane_now()
 #define PT_TID (wave * 64 + lane_now())
-#else
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-#define PT_LANE lane
-#define PT_TID threadIdx.x
-#endif
     const LaunchParams* P0 = params;
     // workgroup copies in LDS: the first mesh ranges, every material and every sphere (the launch
     // reserves their bytes of dynamic LDS; pass_kernel_u runs only when that fits, PT_LDS_TABLES)
     __shared__ int2 lds_mesh[PT_LDS_MESHES];
     __shared__ int4 lds_next[PT_LDS_MESHES + 1];
     __shared__ float4 lds_root[2 * PT_ROOT_MESHES];
-#if PT_GEN_RING
     __shared__ float4 lds_ring[PT_UBLOCK / 64][2 * PT_RING];  // one generation ring per wave
     float4* ring = lds_ring[wave];
     int ring_head = 0, ring_end = 0;  // wave-uniform: entries [ring_head, ring_end) are generated, not yet taken
@@ -426,7 +386,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     // VGPR it was spilled to scratch around the ring fill (written back after every shading batch: 0.6 GB of
     // scratch writes per launch)
     __shared__ unsigned int lds_unit[PT_UBLOCK];
-#endif
     extern __shared__ float4 lds_dyn[];
     DevMaterial* lds_mats = reinterpret_cast<DevMaterial*>(lds_dyn);
     {
@@ -464,7 +423,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     MeshWalk w;
     int mesh = 0;
     int ptri = -1;  // leaf triangle awaiting its test (LANE_TRI)
-    unsigned int unit = 0;
     int32_t pseed = 0;
     int depth = 0;
     int mode = LANE_WANT;
@@ -488,26 +446,14 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
     if (PROF) t_start = __builtin_amdgcn_s_memrealtime();
     while (true) {
         const LaunchParams* P = params;
-#if PT_PARAM_RELOAD
-        asm volatile("" : "+s"(P));
-#endif
+        asm volatile("" : "+s"(P));  // the parameter block's address reloaded each round, not held across it
         P = uniform_ptr(P);
         DevScene sc = load_const(&P->sc);
         sc.materials = lds_mats;
         sc.spheres = lds_spheres;
-#if PT_PARAM_LAZY
-#if PT_PARAM_LAZY == 2
-        const DevConfig cfg = load_const(&P->cfg);
-#else
         const DevConfig& cfg = const_ref(&P->cfg);
-#endif
         const DevTiling& til = const_ref(&P->til);
         const DevOutput& out = const_ref(&P->out);
-#else
-        const DevConfig cfg = load_const(&P->cfg);
-        const DevTiling til = load_const(&P->til);
-        const DevOutput out = load_const(&P->out);
-#endif
         const bool roots = sc.mesh_num <= PT_ROOT_MESHES;  // wave-uniform
         if (PROF) {
             prof[0]++;
@@ -518,7 +464,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
         // lanes without a path take the next (pixel, pass) units, one atomic per wave (pt_work.h)
         const bool want = mode == LANE_WANT;
         const unsigned long long need_mask = __ballot(want);
-#if PT_GEN_RING
         if (need_mask) {
             // lanes take generated paths from the ring in lane order; when it runs dry the wave fetches the next
             // chunk and generates all of it (gen_ring_fill below), then the remaining lanes take from the new ring
@@ -533,8 +478,9 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             }
             if (taken <= avail) {
                 ring_head += taken;
-            } else if (!drained && work_fetch(out.fetch, regions.stride, regions, (unsigned int)chunk, cursor)) {
-                const int n = (int)(cursor.end - cursor.cur);  // <= chunk <= PT_RING (host-checked)
+            } else if (!drained && work_fetch(out.fetch, regions.stride, regions, (unsigned int)min(chunk, PT_RING),
+                                              cursor)) {
+                const int n = (int)(cursor.end - cursor.cur);  // <= min(chunk, PT_RING): the ring's bound, on the device
                 if (PROF) { prof[7] += (unsigned long long)n; gen_batches++; }
                 // gen_ring_fill: lane i generates unit cursor.cur + i. The camera is read through the scalar cache,
                 // so a chunk that spans frames (MULTI) is generated one frame at a time
@@ -554,12 +500,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                             const int32_t hseed = hash_pt(first_pass + (int)(lu & ((1u << batch_log2) - 1u)));
                             const DevCamera cam = MULTI ? load_const(out.cams + f) : load_const(&P->cam);
                             PathState g;
-                            if (PT_DUP == 4) {
-                                PathState p2; int px2 = pixel, hs2 = hseed;
-                                opaque(px2); opaque(hs2);
-                                generate_path(cam, cfg, px2, hs2, &p2);
-                                opaque(p2);
-                            }
                             generate_path(cam, cfg, pixel, hseed, &g);
                             gen_ring_put(ring, PT_LANE, g, path_seed(hseed, pixel), gu);
                         }
@@ -594,74 +534,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
                 }
             }
         }
-#else
-        if (need_mask) {
-            const unsigned int u = work_take(out.fetch, regions.stride, regions, (unsigned int)chunk, need_mask, want,
-                                             lanes_below(PT_LANE), cursor, drained);
-            if (PROF) {
-                const unsigned long long started = __ballot(want && u != ~0u);
-                prof[7] += (unsigned long long)__popcll(started);
-                gen_batches += started ? 1ull : 0ull;
-            }
-            if (PROF && drained && t_drain == 0) t_drain = __builtin_amdgcn_s_memrealtime();
-            if (want) {
-                if (u != ~0u) {
-                    unit = u;
-                    if (MULTI) {
-                        mode = LANE_GEN;
-                    } else {
-                        const int pixel = unit_to_pixel(til, u >> batch_log2);
-                        const int32_t hseed = hash_pt(first_pass + (int)(u & ((1u << batch_log2) - 1u)));
-                        const DevCamera cam = load_const(&P->cam);
-                        if (PT_DUP == 4) {
-                            PathState p2; int px2 = pixel, hs2 = hseed;
-                            opaque(px2); opaque(hs2);
-                            generate_path(cam, cfg, px2, hs2, &p2);
-                            opaque(p2);
-                        }
-                        generate_path(cam, cfg, pixel, hseed, &ps);
-                        pseed = path_seed(hseed, pixel);
-                        depth = 0;
-                        if (cfg.max_depth > 0) {
-                            mode = LANE_NEW;
-                        } else {
-                            finish_unit(til, cfg, out, ps, unit, 0u, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
-                        }
-                    }
-                } else if (drained) {
-                    mode = LANE_DONE;
-                }
-            }
-        }
-#if !PT_GEN_RING
-        // MULTI: lanes holding a new unit start its camera path. The camera is read through the scalar cache, so
-        // one refill starts the paths of one frame: those of the first such lane's frame; a lane whose unit lies
-        // in another frame (a refill that spans two frames' units) starts in the next round
-        const unsigned long long gen_mask = MULTI ? __ballot(mode == LANE_GEN) : 0ull;
-        if (MULTI && gen_mask) {
-            unsigned int lu = unit;  // the unit within its frame
-            int frame = 0;
-            if (mode == LANE_GEN) {
-                while (lu >= frame_units) { lu -= frame_units; frame++; }
-            }
-            const int f0 = __builtin_amdgcn_readlane(frame, (int)__builtin_ctzll(gen_mask));
-            if (mode == LANE_GEN && frame == f0) {
-                const int pixel = unit_to_pixel(til, lu >> batch_log2);
-                const int32_t hseed = hash_pt(first_pass + (int)(lu & ((1u << batch_log2) - 1u)));
-                const DevCamera cam = load_const(out.cams + f0);
-                generate_path(cam, cfg, pixel, hseed, &ps);
-                pseed = path_seed(hseed, pixel);
-                depth = 0;
-                if (cfg.max_depth > 0) {
-                    mode = LANE_NEW;
-                } else {
-                    finish_unit(til, cfg, out, ps, unit, frame_units, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
-                    mode = LANE_WANT;
-                }
-            }
-        }
-#endif
-#endif
         if (mode == LANE_NEW) {
             if (FEAT & PT_FEAT_MBOUND) {
                 wbound = medium_bound(sc, cfg, ps.medium, depth, pseed);
@@ -682,23 +554,13 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             bool alive = false;
             if (mode == LANE_READY) {
                 // the rest of trace_ray_kernel for this segment (:456-624)
-                if (PT_DUP == 1) {
-                    PathState p2 = ps; Hit h2 = h; int d2 = depth;
-                    opaque(p2); opaque(h2); opaque(d2);
-                    bool a2 = shade_hit<false, FEAT>(sc, cfg, d2, pseed, &p2, h2, &none, nullptr);
-                    opaque(p2); opaque(a2);
-                }
                 alive = shade_hit<false, FEAT>(sc, cfg, depth, pseed, &ps, h, &none, nullptr);
             }
             if (PROF) tc2 = __builtin_readcyclecounter();
             if (mode == LANE_READY) {  // the pass's end for this unit, or the next trace step
                 depth++;
                 if (!alive || depth >= cfg.max_depth) {
-#if PT_GEN_RING
                     const unsigned int un = lds_unit[PT_TID];
-#else
-                    const unsigned int un = unit;
-#endif
                     finish_unit(til, cfg, out, ps, un, MULTI ? frame_units : 0u, first_pass, write_u8, batch_log2, (float)cfg.max_depth * 2.0f, depth);
                     mode = LANE_WANT;
                 } else {
@@ -740,24 +602,11 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (PROF) {
                 prof[1]++; prof[2] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK));
                 prof[12] += (unsigned long long)__popcll(__ballot(mode == LANE_TRI));
-#if PT_PROF_MESH  // diagnostic builds: walking lanes per mesh (meshes 0, 1, 2) instead of the drained/ready/idle counts
-                prof[11] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK && (mesh & 0xff) == 0));
-                prof[13] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK && (mesh & 0xff) == 1));
-                prof[14] += (unsigned long long)__popcll(__ballot(mode == LANE_WALK && (mesh & 0xff) == 2));
-#else
                 if (drained) prof[11] += 1ull | ((unsigned long long)__popcll(__ballot(mode == LANE_WALK)) << 32);
                 prof[13] += (unsigned long long)__popcll(__ballot(mode == LANE_READY));
                 prof[14] += (unsigned long long)__popcll(__ballot(mode == LANE_WANT || mode == LANE_DONE));
-#endif
             }
             if (mode == LANE_WALK) {
-                if (PT_DUP == 2) {
-                    MeshWalk w2 = w; v3 o2 = ps.o, i2 = inv; int t2 = ptri;
-                    opaque(w2); opaque(o2); opaque(i2);
-                    float4 a2, b2, c2;
-                    bool l2 = walk_box_inline(rn, o2, i2, w2, t2, a2, b2, c2);
-                    opaque(w2); opaque(l2); opaque(t2); opaque(a2); opaque(b2); opaque(c2);
-                }
                 // a leaf whose box passes: the lane parks with its triangle, which came with the step's records
                 if (PT_WALK_PRIO) __builtin_amdgcn_s_setprio(PT_WALK_PRIO);  // until the step's loads issue (pt_path.h)
                 if (walk_box_inline(rn, ps.o, inv, w, ptri, pta, ptb, ptc)) mode = LANE_TRI;
@@ -769,12 +618,6 @@ __global__ __launch_bounds__(PT_UBLOCK, MINW) void pass_kernel_u(const LaunchPar
             if (pend && (__popcll(pend) >= (unsigned int)tri_min || !__any(mode == LANE_WALK) || k == walk_steps - 1)) {
                 if (PROF) { prof[5]++; prof[6] += (unsigned long long)__popcll(pend); }
                 if (mode == LANE_TRI) {
-                    if (PT_DUP == 3) {
-                        MeshWalk w2 = w; v3 o2 = ps.o, d2 = ps.d; float4 a2 = pta, b2 = ptb, c2 = ptc; int t2 = ptri;
-                        opaque(w2); opaque(o2); opaque(d2); opaque(a2); opaque(b2); opaque(c2); opaque(t2);
-                        walk_tri_geom(a2, b2, c2, o2, d2, w2, t2);
-                        opaque(w2);
-                    }
                     walk_tri_geom(pta, ptb, ptc, ps.o, ps.d, w, ptri);
                     w.pos++;  // past the leaf's triangle record too
                     mode = LANE_WALK;
@@ -862,27 +705,58 @@ __global__ __launch_bounds__(PT_BLOCK) void accumulate_frames_kernel(const Launc
 // One pass of a batched launch added into the running sum: pass `pass` is slot j of every unit's run of
 // 2^batch_log2 pass radiances in rad (path_tracer_kernel.cu:644-651 for that pass), then its 8-bit output.
 // The reference ABI's pass cache (pt_runtime.cpp abi_render_pass) serves one pass per call this way.
+// src: the running sum the pass adds into (null: the image itself, in place); the reference ABI keeps the
+// caller's uploaded sum apart so that a call can be redone (pt_runtime.cpp path_tracer_kernel).
 __global__ __launch_bounds__(PT_BLOCK) void accumulate_one_kernel(const LaunchParams* __restrict__ P, int pass,
                                                                   int batch_log2, int j, int write_u8,
-                                                                  const float* __restrict__ rad, int unit_begin,
-                                                                  int unit_end) {
+                                                                  const float* __restrict__ rad, const float* src,
+                                                                  int unit_begin, int unit_end) {
     const unsigned int lu = unit_begin + blockIdx.x * PT_BLOCK + threadIdx.x;
     if (lu >= (unsigned int)unit_end) return;
     const int pixel = unit_to_pixel(P->til, lu);
     float* img = P->out.image + (size_t)pixel * 3;
+    const float* old = (src ? src : P->out.image) + (size_t)pixel * 3;
     const float* pr = rad + (((size_t)lu << batch_log2) + (size_t)j) * 3;
     const v3 c = mk3(pr[0], pr[1], pr[2]);
-    const v3 sum = pass == 1 ? c : mk3(img[0], img[1], img[2]) + c;
+    const v3 sum = pass == 1 ? c : mk3(old[0], old[1], old[2]) + c;
     img[0] = sum.x; img[1] = sum.y; img[2] = sum.z;
     if (write_u8 && P->out.image256) store_u8(P->cfg, sum, pass, P->out.image256 + (size_t)pixel * 3);
 }
 
 hipError_t launch_accumulate_one(const LaunchParams* params_dev, int unit_begin, int unit_end, int pass, int batch_log2,
-                                 int j, int write_u8, const float* rad, hipStream_t stream) {
+                                 int j, int write_u8, const float* rad, const float* src, hipStream_t stream) {
     const int units = unit_end - unit_begin;
     if (units <= 0) return hipSuccess;
     hipLaunchKernelGGL(accumulate_one_kernel, dim3((units + PT_BLOCK - 1) / PT_BLOCK), dim3(PT_BLOCK), 0, stream,
-                       params_dev, pass, batch_log2, j, write_u8, rad, unit_begin, unit_end);
+                       params_dev, pass, batch_log2, j, write_u8, rad, src, unit_begin, unit_end);
+    return hipGetLastError();
+}
+
+// An order-independent 64-bit digest of words [begin, end) of a buffer, added into *out: the sum over words of
+// splitmix64((index << 32) | word) (wrapping). The reference ABI digests the running sum it returns and the one the
+// caller hands back, so it can tell that passes ran elsewhere in between (pt_runtime.cpp path_tracer_kernel).
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(PT_BLOCK) void digest_words_kernel(const uint32_t* __restrict__ p, unsigned long long begin,
+                                                                unsigned long long end, unsigned long long* out) {
+    unsigned long long h = 0;
+    const unsigned long long stride = (unsigned long long)gridDim.x * PT_BLOCK;
+    for (unsigned long long i = begin + blockIdx.x * PT_BLOCK + threadIdx.x; i < end; i += stride)
+        h += splitmix64((i << 32) | p[i]);
+    for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, h);
+}
+
+hipError_t launch_digest_words(const void* p, size_t begin, size_t end, unsigned long long* out, hipStream_t stream) {
+    if (end <= begin) return hipSuccess;
+    const size_t blocks = std::min<size_t>((end - begin + PT_BLOCK - 1) / PT_BLOCK, 2048);
+    hipLaunchKernelGGL(digest_words_kernel, dim3((unsigned)blocks), dim3(PT_BLOCK), 0, stream,
+                       static_cast<const uint32_t*>(p), (unsigned long long)begin, (unsigned long long)end, out);
     return hipGetLastError();
 }
 
@@ -1222,7 +1096,7 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
         // +0.4 %, C3 +0.9 %, C4/C5 +0.1-0.3 %, profiles/r03/walk_steps/; 4 parked lanes instead of 6 since the
         // fused multiply-adds made the triangle test cheaper: +0.3 % over four rounds, profiles/r04/knobs/)
         // (the generation ring holds one chunk: 1..64 units)
-        static const int chunk = PT_GEN_RING ? env_int("PT_CHUNK_MEGA", 64, 1, PT_RING) : env_int("PT_CHUNK_MEGA", 64, 0, 4096);
+        static const int chunk = env_int("PT_CHUNK_MEGA", 64, 1, PT_RING);
         // the shading batch waits for 40 ready lanes with a medium walked exactly (the medium step makes a batch
         // dearer: C4 5952-5966 vs 5747 Mrays/s, 36: 5936-5952, 44: 5814, profiles/r04/knobs/c4_c5_shade_min.txt),
         // 28 otherwise (C5 at 32 / 36: ±0 / -1 %; the medium-bounded walk, shorter: 9450 at 40 vs 9573-9597)

@@ -552,6 +552,16 @@ struct pt_context {
     hipEvent_t spec_done[2] = {nullptr, nullptr};
     hipStream_t acc_stream = nullptr;  // the ABI's per-call accumulate and download
     hipEvent_t chunk_up[4] = {nullptr, nullptr, nullptr, nullptr};  // the running sum's upload, per chunk
+    // the reference ABI on host-visible images: a continuation call's copy of the caller's running sum (kept apart
+    // from the result, so the call can be redone on an edited scene) and digests (launch_digest_words) of the sum a
+    // call received ([0]) and returned ([1]). A received sum that is not the one the last call returned means that
+    // passes ran elsewhere in between — the caller's CPU twin, after an in-place edit this library never saw —
+    // even when the pass counter continues this library's own (Core/path_tracer.cpp:46-91, window.cpp:580-588).
+    float* caller_sum = nullptr;
+    size_t caller_sum_cap = 0;
+    unsigned long long* sum_digest = nullptr;
+    unsigned long long ret_digest = 0;
+    bool ret_digest_valid = false;
     std::vector<int2> mesh_range;  // node range per mesh of the resident scene
     // one triangle per leaf: the inline-leaf node array pass_kernel_u walks (pt_path.h walk_box_inline),
     // the record map it is built through (np, R + 1 ints), its mesh ranges and first range
@@ -1053,8 +1063,11 @@ int render_passes(pt_context* ctx, const pt_render_camera* cam, const pt_configu
     const int feat = render_feat(ctx, dc);
     const PassChoice pc0 = pass_choice(ctx, feat);
     const int units = ctx->tiling.unit_count;
+    // the largest batch a launch of this call takes: a power of two, at most the call's pass count (pass_rad is
+    // sized for it and kept on the context)
     int most = 1;
-    while (most * 2 <= max_pass_batch() && (long long)units * most * 2 <= (1ll << 28)) most *= 2;
+    while (most * 2 <= max_pass_batch() && most * 2 <= pass_count && (long long)units * most * 2 <= (1ll << 28))
+        most *= 2;
     const bool rad1 = ctx->rad_single;  // one-pass launches write pass_rad and are accumulated afterwards
     if ((most > 1 && pass_count > 1) || rad1) {
         const size_t need = (size_t)units * (size_t)most * 12;
@@ -1123,6 +1136,21 @@ int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, con
     if (prc != PT_OK) return prc;
     for (int f = 1; f < frames; f++)
         if ((int)cams[f].resolution.x != ctx->width) { set_error("camera width != frame width"); return PT_E_ARG; }
+    // every frame's accumulate runs at once (accumulate_frames_kernel, blockIdx.y = frame): the frames' buffers must
+    // not alias one another
+    {
+        std::vector<const void*> seen;
+        seen.reserve((size_t)frames * 2);
+        for (int f = 0; f < frames; f++) {
+            seen.push_back(images[f]);
+            if (images256 && images256[f]) seen.push_back(images256[f]);
+        }
+        std::sort(seen.begin(), seen.end());
+        if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) {
+            set_error("pt_render_frames: two frames share an image buffer");
+            return PT_E_ARG;
+        }
+    }
     const int feat = render_feat(ctx, lp.cfg);
     PassChoice pc = pass_choice(ctx, feat);
     const bool fused = frames > 1 && !wavefront_schedule(ctx) && pass_uses_unified(pc, pass_lds_bytes(ctx)) &&
@@ -1165,8 +1193,10 @@ int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, con
     }
     PT_HIP(hipMemcpyAsync(ctx->cams, host.data(), table_bytes, hipMemcpyHostToDevice, ctx->stream));
     const uint64_t* ptrs_dev = reinterpret_cast<const uint64_t*>(reinterpret_cast<const unsigned char*>(ctx->cams) + cam_bytes);
-    int most = 1;
-    while (most * 2 <= max_pass_batch() && (long long)units * most * 2 * frames <= kMaxFrameLaunchUnits) most *= 2;
+    int most = 1;  // as render_passes: a power of two, at most pass_count
+    while (most * 2 <= max_pass_batch() && most * 2 <= pass_count &&
+           (long long)units * most * 2 * frames <= kMaxFrameLaunchUnits)
+        most *= 2;
     const size_t need = (size_t)units * (size_t)most * (size_t)frames * 12;
     if (need > ctx->pass_rad_bytes) {
         if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
@@ -1311,17 +1341,23 @@ int abi_render_pass(pt_context* ctx, const pt_render_camera* cam, const pt_confi
     PT_HIP(hipMemcpyAsync(ctx->params, &lp, sizeof(lp), hipMemcpyHostToDevice, as));
     const int K = io.direct || io.pageable ? 1 : 4;
     const bool up = !io.direct && pass != 1;  // pass 1 overwrites: nothing to add into
+    // the caller's running sum lands in caller_sum (the accumulate reads it there) and is digested as it arrives;
+    // the result is digested before it goes down (sum_digest, path_tracer_kernel)
+    if (up) PT_HIP(hipMemsetAsync(ctx->sum_digest, 0, sizeof(unsigned long long), ctx->copy_stream));
+    if (!io.direct) PT_HIP(hipMemsetAsync(ctx->sum_digest + 1, 0, sizeof(unsigned long long), as));
     for (int c = 0; c < K; c++) {
         const int b0 = (int)((long long)units * c / K), b1 = (int)((long long)units * (c + 1) / K);
         if (up) {
-            PT_HIP(hipMemcpyAsync(ctx->image + (size_t)b0 * 3, io.img + b0, (size_t)(b1 - b0) * 12, hipMemcpyDefault,
-                                  ctx->copy_stream));
+            PT_HIP(hipMemcpyAsync(ctx->caller_sum + (size_t)b0 * 3, io.img + b0, (size_t)(b1 - b0) * 12,
+                                  hipMemcpyDefault, ctx->copy_stream));
+            PT_HIP(launch_digest_words(ctx->caller_sum, (size_t)b0 * 3, (size_t)b1 * 3, ctx->sum_digest, ctx->copy_stream));
             PT_HIP(hipEventRecord(ctx->chunk_up[c], ctx->copy_stream));
             PT_HIP(hipStreamWaitEvent(as, ctx->chunk_up[c], 0));
         }
         PT_HIP(launch_accumulate_one(ctx->params, b0, b1, pass, ctx->spec_lg, pass - ctx->spec_first[slot], 1,
-                                     ctx->spec_rad[slot], as));
+                                     ctx->spec_rad[slot], up ? ctx->caller_sum : nullptr, as));
         if (!io.direct) {
+            PT_HIP(launch_digest_words(ctx->image, (size_t)b0 * 3, (size_t)b1 * 3, ctx->sum_digest + 1, as));
             PT_HIP(hipMemcpyAsync(io.img + b0, ctx->image + (size_t)b0 * 3, (size_t)(b1 - b0) * 12, hipMemcpyDefault, as));
             PT_HIP(hipMemcpyAsync(io.img8 + b0, ctx->image256 + (size_t)b0 * 3, (size_t)(b1 - b0) * 3, hipMemcpyDefault, as));
         }
@@ -1423,6 +1459,8 @@ extern "C" void pt_context_destroy(pt_context* ctx) {
     if (ctx->wave_mem) (void)hipFree(ctx->wave_mem);
     if (ctx->pass_rad) (void)hipFree(ctx->pass_rad);
     if (ctx->cams) (void)hipFree(ctx->cams);
+    if (ctx->caller_sum) (void)hipFree(ctx->caller_sum);
+    if (ctx->sum_digest) (void)hipFree(ctx->sum_digest);
     for (int k = 0; k < 2; k++) {
         if (ctx->spec_rad[k]) (void)hipFree(ctx->spec_rad[k]);
         if (ctx->spec_params[k]) (void)hipFree(ctx->spec_params[k]);
@@ -1859,11 +1897,33 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
     ctx->tiling.band_count = 1;
     ctx->tiling.band_index = 0;
     const size_t px = (size_t)pixel_count;
+    if (!direct) {  // the caller's running sum is kept apart and digested (pt_context::caller_sum, sum_digest)
+        hipError_t e = hipSuccess;
+        if (ctx->caller_sum_cap < px * 3) {
+            if (ctx->caller_sum) (void)hipFree(ctx->caller_sum);
+            ctx->caller_sum = nullptr;
+            ctx->caller_sum_cap = 0;
+            e = hipMalloc(&ctx->caller_sum, px * 12);
+            if (e == hipSuccess) ctx->caller_sum_cap = px * 3;
+        }
+        if (e == hipSuccess && !ctx->sum_digest) e = hipMalloc(&ctx->sum_digest, 2 * sizeof(unsigned long long));
+        if (e != hipSuccess) {
+            set_error("[Hip]Error %s allocating the running-sum copy", hipGetErrorString(e));
+            report("path_tracer_kernel: image");
+            return;
+        }
+    }
     if (!direct && pass_counter != 1) {
         // enqueued by render_passes right after the pass kernel (a copy from pageable memory can hold the
-        // host until it is done, so it must not come before the launch)
+        // host until it is done, so it must not come before the launch): the caller's sum goes to caller_sum, is
+        // digested, and is copied into the image the pass adds into
         ctx->before_acc = [ctx, image_pixels, px]() -> int {
-            hipError_t e = hipMemcpyAsync(ctx->image, image_pixels, px * 12, hipMemcpyDefault, ctx->copy_stream);
+            hipError_t e = hipMemsetAsync(ctx->sum_digest, 0, sizeof(unsigned long long), ctx->copy_stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(ctx->caller_sum, image_pixels, px * 12, hipMemcpyDefault, ctx->copy_stream);
+            if (e == hipSuccess) e = launch_digest_words(ctx->caller_sum, 0, px * 3, ctx->sum_digest, ctx->copy_stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(ctx->image, ctx->caller_sum, px * 12, hipMemcpyDeviceToDevice, ctx->copy_stream);
             if (e == hipSuccess) e = hipEventRecord(ctx->copy_done, ctx->copy_stream);
             if (e != hipSuccess) { set_error("[Hip]Error uploading the caller's running sum"); return PT_E_HIP; }
             ctx->acc_wait = ctx->copy_done;
@@ -1946,22 +2006,61 @@ extern "C" void path_tracer_kernel(int mesh_num, pt_bvh_node_device** bvh_nodes_
         }
     }
     const double t_launch = ms();
-    if (rc == PT_OK) {
-        if (!direct && downloaded) {
-            if (hipStreamSynchronize(done) != hipSuccess) { set_error("[Hip]Error synchronize"); rc = PT_E_HIP; }
-        } else if (!direct) {
-            hipError_t e = hipMemcpyAsync(image_pixels, ctx->image, px * 12, hipMemcpyDefault, done);
-            if (e == hipSuccess) e = hipMemcpyAsync(image_pixels_256, ctx->image256, px * 3, hipMemcpyDefault, done);
-            if (e == hipSuccess) e = hipStreamSynchronize(done);
-            if (e != hipSuccess) { set_error("[Hip]Error %s downloading the image", hipGetErrorString(e)); rc = PT_E_HIP; }
-        } else if (hipStreamSynchronize(done) != hipSuccess) {
-            set_error("[Hip]Error synchronize");
+    // the result goes down to a host-visible image (digested first, sum_digest[1]), then the call waits for it
+    auto finish = [&]() {
+        if (rc == PT_OK) {
+            if (!direct && downloaded) {
+                if (hipStreamSynchronize(done) != hipSuccess) { set_error("[Hip]Error synchronize"); rc = PT_E_HIP; }
+            } else if (!direct) {
+                hipError_t e = hipMemsetAsync(ctx->sum_digest + 1, 0, sizeof(unsigned long long), done);
+                if (e == hipSuccess) e = launch_digest_words(ctx->image, 0, px * 3, ctx->sum_digest + 1, done);
+                if (e == hipSuccess) e = hipMemcpyAsync(image_pixels, ctx->image, px * 12, hipMemcpyDefault, done);
+                if (e == hipSuccess) e = hipMemcpyAsync(image_pixels_256, ctx->image256, px * 3, hipMemcpyDefault, done);
+                if (e == hipSuccess) e = hipStreamSynchronize(done);
+                if (e != hipSuccess) { set_error("[Hip]Error %s downloading the image", hipGetErrorString(e)); rc = PT_E_HIP; }
+            } else if (hipStreamSynchronize(done) != hipSuccess) {
+                set_error("[Hip]Error synchronize");
+                rc = PT_E_HIP;
+            }
+        } else {
+            (void)hipStreamSynchronize(done);
+            (void)hipStreamSynchronize(ctx->stream);
+        }
+    };
+    finish();
+    unsigned long long dig[2] = {0, 0};
+    if (rc == PT_OK && !direct) {
+        (void)hipStreamSynchronize(ctx->copy_stream);
+        if (hipMemcpy(dig, ctx->sum_digest, sizeof(dig), hipMemcpyDeviceToHost) != hipSuccess) {
+            set_error("[Hip]Error reading the running-sum digests");
             rc = PT_E_HIP;
         }
-    } else {
-        (void)hipStreamSynchronize(done);
-        (void)hipStreamSynchronize(ctx->stream);
     }
+    // A continuation whose running sum is not the one this library returned last: passes ran elsewhere (the CPU
+    // twin) although the counter continues this library's own (GPU passes 1..k, an in-place edit, CPU-twin passes
+    // 1..k, then this call at k + 1). The caller's scene is checked now; if it changed, this call is redone on the
+    // new scene from the caller's sum (kept in caller_sum) and returned again.
+    if (rc == PT_OK && !direct && pass_counter != 1 && !gap && ctx->ret_digest_valid && dig[0] != ctx->ret_digest) {
+        rd_ok = abi_scene_digest(mesh_num, bvh_nodes_device, triangles_device, sphere_num, spheres_device,
+                                 sky_cube_map_device, mesh_textures_device, &config, &rd);
+        if (!(rd_ok && ctx->raw_valid && ctx->raw == rd)) {
+            upload(rd, rd_ok);
+            if (rc == PT_OK) {
+                hipError_t e = hipMemcpyAsync(ctx->image, ctx->caller_sum, px * 12, hipMemcpyDeviceToDevice, ctx->stream);
+                if (e != hipSuccess) { set_error("[Hip]Error %s restoring the running sum", hipGetErrorString(e)); rc = PT_E_HIP; }
+            }
+            if (rc == PT_OK) rc = render_passes(ctx, &cam, &config, pass_counter, 1, 1);
+            done = ctx->stream;
+            downloaded = false;
+            finish();
+            if (rc == PT_OK && hipMemcpy(dig + 1, ctx->sum_digest + 1, sizeof(dig[1]), hipMemcpyDeviceToHost) != hipSuccess) {
+                set_error("[Hip]Error reading the running-sum digest");
+                rc = PT_E_HIP;
+            }
+        }
+    }
+    ctx->ret_digest = dig[1];
+    ctx->ret_digest_valid = rc == PT_OK && !direct;
     if (direct) { ctx->image256 = own256; ctx->image = nullptr; ctx->image_cap = 0; ctx->own_image = false; }
     ctx->abi_last_pass = rc == PT_OK ? pass_counter : 0;
     if (timing)

@@ -43,6 +43,50 @@ def owned_pixels(width: int, height: int, band_rows: int, band_count: int, band_
     return (rows[:, None] * width + np.arange(width)[None, :]).reshape(-1).astype(np.int32)
 
 
+class StageClock:
+    """Per launch of a TiledFrame / FrameGroup: when it started, when its passes were rendered and when its collective
+    was done, as HIP events on the renderer's stream (a CUDA frame) or host clock readings (a host-side renderer, whose
+    steps run in host order). timings() gives (render_ms, collective_ms) per launch since the last reset():
+    bench.py's per-rank breakdown of a multi-GPU run."""
+
+    def __init__(self, stream=None):
+        self.stream = stream
+        self.marks: list[list] = []
+
+    def reset(self) -> None:
+        self.marks = []
+
+    def _now(self):
+        if self.stream is None:
+            import time
+
+            return time.perf_counter()
+        import torch
+
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(self.stream)
+        return ev
+
+    def start(self) -> None:
+        self.marks.append([self._now()])
+
+    def mark(self) -> None:
+        if self.marks:
+            self.marks[-1].append(self._now())
+
+    def timings(self) -> list[tuple[float, float]]:
+        out = []
+        for m in self.marks:
+            if len(m) != 3:
+                continue
+            if self.stream is None:
+                out.append(((m[1] - m[0]) * 1e3, (m[2] - m[1]) * 1e3))
+            else:
+                m[2].synchronize()
+                out.append((m[0].elapsed_time(m[1]), m[1].elapsed_time(m[2])))
+        return out
+
+
 def _placement(rows, most: int, device):
     """Where the gather's landing rows go on rank 0: row i of rank k's piece (k >= 1) is landing row
     k * most + i and frame row rows[k][i] (rank 0's own rows are rendered in place). Empty for one rank."""
@@ -96,6 +140,7 @@ class TiledFrame:
                 self.stream = torch.cuda.ExternalStream(renderer.stream_handle(), device=self.image.device)
         else:
             renderer.setup_frame(width, height)
+        self.clock = StageClock(self.stream)
 
     def _on_stream(self):
         """Torch work of the frame goes on the renderer's stream (in order with its passes)."""
@@ -116,6 +161,7 @@ class TiledFrame:
             self.r.render(cam, cfg, 1, spp, write_u8=2)
             return
         with self._on_stream():
+            self.clock.start()
             if self.collective == "reduce":
                 # rows outside this rank's bands must be zero for the reduce, and rank 0's buffer still
                 # holds the previous frame's sum: clear it (ordered before the passes on this stream)
@@ -123,6 +169,7 @@ class TiledFrame:
             self.r.render(cam, cfg, 1, spp, write_u8=0)
             if self.stream is None:
                 self.r.synchronize()
+            self.clock.mark()
             if self.collective == "reduce":
                 self.dist.reduce(self.image, dst=0)  # the one collective of the frame
             else:
@@ -132,6 +179,7 @@ class TiledFrame:
                 self.dist.gather(self.part, gather_list=self.parts, dst=0)  # the one collective of the frame
                 if self.rank == 0:
                     img[self.dst_rows] = self.landing.view(-1, self.width, 3)[self.src_rows]
+            self.clock.mark()
             if self.rank == 0:
                 self.r.finalize_u8(cfg, spp)
 
@@ -208,6 +256,7 @@ class FrameGroup:
                 self.src_rows, self.dst_rows = _placement(self.rows, most, device)
         if self.stack.is_cuda and hasattr(renderer, "stream_handle"):
             self.stream = torch.cuda.ExternalStream(renderer.stream_handle(), device=self.stack.device)
+        self.clock = StageClock(self.stream)
 
     def _on_stream(self):
         import contextlib
@@ -231,12 +280,15 @@ class FrameGroup:
                 self.r.render_frames(list(cams), cfg, self.images[:n], self.images8[:n], 1, spp, write_u8=2)
             return
         with self._on_stream():
+            self.clock.start()
             if self.collective == "reduce":
                 self.stack[:n].zero_()  # rows outside this rank's bands must be zero for the reduce
                 self.r.render_frames(list(cams), cfg, self.images[:n], None, 1, spp, write_u8=0)
                 if self.stream is None:
                     self.r.synchronize()
+                self.clock.mark()
                 self.dist.reduce(self.stack, dst=0)  # the one collective of the group
+                self.clock.mark()
                 if self.rank == 0:
                     for f in range(n):
                         self.r.finalize_u8_image(cfg, spp, self.images[f], self.images8[f])
@@ -244,9 +296,11 @@ class FrameGroup:
             self.r.render_frames(list(cams), cfg, self.images[:n], self.images8[:n], 1, spp, write_u8=2)
             if self.stream is None:
                 self.r.synchronize()
+            self.clock.mark()
             if self.collective == "gather":
                 self._gather_rows(self.stack, self.part, self.parts, self.landing if self.rank == 0 else None, n)
             self._gather_rows(self.stack8, self.part8, self.parts8, self.landing8 if self.rank == 0 else None, n)
+            self.clock.mark()
 
     def _gather_rows(self, stack, part, parts, landing, n: int) -> None:
         """Frames 0..n-1 of `stack`: every rank's own rows to rank 0 (one gather of n frames' pieces; a launch of
@@ -283,3 +337,41 @@ class FrameGroup:
         shape = (self.height, self.width, 3)
         return (self.stack[frame].cpu().numpy().reshape(shape).copy(),
                 self.stack8[frame].cpu().numpy().reshape(shape).copy())
+
+
+class StageWatch:
+    """Fail-fast for one rank of a multi-GPU run: the rank names the stage it is in (stage()), and a watchdog thread
+    ends the process when a stage outlives its limit, with one stderr line naming the rank and the stage, and exit
+    code 124. A rank whose peer never reaches a collective (a stalled or lost rank) thus exits non-zero on its own
+    instead of waiting for the job's outer time limit, and torch.distributed.run then ends the other ranks. The
+    thread only reads a clock: it works while the main thread is blocked in a collective or a device wait (those
+    release the GIL)."""
+
+    def __init__(self, rank: int, limit_s: float, tag: str = "[bench]", exit_code: int = 124):
+        import threading
+        import time
+
+        self.rank, self.limit_s, self.tag, self.exit_code = rank, float(limit_s), tag, exit_code
+        self._time = time.monotonic
+        self._name, self._since, self._limit = "start", self._time(), self.limit_s
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._watch, name="stage-watch", daemon=True)
+        if self.limit_s > 0:
+            self._thread.start()
+
+    def stage(self, name: str, limit_s: float | None = None) -> None:
+        self._name, self._since = name, self._time()
+        self._limit = self.limit_s if limit_s is None else float(limit_s)
+
+    def _watch(self) -> None:
+        import sys
+
+        while not self._stop.wait(0.25):
+            waited = self._time() - self._since
+            if waited > self._limit:
+                print(f"{self.tag} rank {self.rank}: stage '{self._name}' did not finish within {self._limit:.0f} s "
+                      f"({waited:.1f} s); exiting with {self.exit_code}", file=sys.stderr, flush=True)
+                os._exit(self.exit_code)
+
+    def close(self) -> None:
+        self._stop.set()

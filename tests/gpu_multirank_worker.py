@@ -7,7 +7,11 @@ context's float image and 8-bit image for the test to compare with the oracle.
 With GROUP > 1 every context is a FrameGroup: each launch renders GROUP frames, frame j through the camera
 turned by yaw 0.3 j (GROUP cameras), moved by one collective; rank 0 saves every frame of every context.
 
-    worker.py OUT_PREFIX COLLECTIVE LAUNCHES [INFLIGHT [GROUP]]
+With CONTINUE ("continue", gather8 groups only): after the groups, every rank gathers the float rows (collect_float),
+and rank 0 alone carries on accumulating frame 0 of its first context, passes SPP+1 .. 2 SPP over the whole frame
+(untiled) into that running sum, as a caller adding passes to the image it was handed would; it saves that sum.
+
+    worker.py OUT_PREFIX COLLECTIVE LAUNCHES [INFLIGHT [GROUP [CONTINUE]]]
 """
 import os
 import sys
@@ -30,6 +34,7 @@ def main() -> int:
     out, collective, frames = sys.argv[1], sys.argv[2], int(sys.argv[3])
     inflight = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     group = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+    cont = len(sys.argv) > 6 and sys.argv[6] == "continue"
     share = 100 // (inflight - 1) if inflight >= 3 else 100
     import torch.distributed as dist
 
@@ -73,6 +78,17 @@ def main() -> int:
                 _, img8 = r.download()
                 np.save(f"{out}_{k}_f.npy", f.image.cpu().numpy().reshape(-1, 3))
                 np.save(f"{out}_{k}_u8.npy", img8.reshape(-1, 3))
+    if cont and rank == 0:
+        # gather8 left each rank's float rows on that rank; collect_float (above) brought them to rank 0. Now the
+        # caller continues frame 0 on rank 0 alone, untiled: passes SPP+1 .. 2 SPP add into the collected sum
+        r, f = rs[0], fr[0]
+        r.set_tiling(8, 1, 0)
+        r.setup_frame(W, H, f.images[0].data_ptr())
+        r.render(cams[0], cfg, SPP + 1, SPP, write_u8=2)
+        r.synchronize()
+        _, img8 = r.download()
+        np.save(f"{out}_cont_f.npy", f.images[0].cpu().numpy().reshape(-1, 3))
+        np.save(f"{out}_cont_u8.npy", img8.reshape(-1, 3))
     dist.barrier()
     for r in rs:
         r.close()

@@ -171,3 +171,59 @@ def test_random_reference_abi_sequences_equal_the_oracle(require_gpu):
     run()
     assert calls["gpu"] >= 200, calls
     assert calls["cpu"] >= 10 and calls["kinds"] == {"host", "managed", "device"}, calls
+
+
+@pytest.mark.parametrize("kind", ["host", "managed"])
+@pytest.mark.parametrize("edit", [True, False])
+def test_cpu_twin_pass_run_after_an_edit_is_seen_at_a_continuing_counter(require_gpu, kind, edit):
+    """The F2 sequence the pass counter cannot reveal (advisor r05): GPU passes 1-2, an in-place edit (its pass-1
+    reset), CPU-twin passes 1-2 on the same buffers, then the GPU again at pass 3, which continues the library's own
+    last pass. The running sum the caller hands over is not the one the library returned, so the library checks the
+    scene and, after an edit, redoes the call on the edited scene (its render-ahead held pass 3 of the old one).
+    Without the edit the check finds the same scene and keeps the cached pass."""
+    hip = _hip()
+    lib = pt.lib()
+    n = W * H
+    sc = pt.cornell_scene(pt.torus_knot(40, 12), cube_length=16)
+    v = sc.view
+    cfg = pt.configuration(max_tracer_depth=5)
+    cam = pt.camera(W, H, **CAM)
+    img = Images(hip, kind, n)
+    scratch = [C.c_void_p() for _ in range(5)]
+    lib.path_tracer_kernel_memory_allocate(*[C.byref(s) for s in scratch], n)
+    want = np.zeros((n, 3), np.float32)
+    want8 = np.zeros((n, 3), np.uint8)
+
+    def gpu(p):
+        lib.path_tracer_kernel(v.mesh_num, v.bvh_nodes, v.triangles, v.sphere_num, v.spheres, n,
+                               C.cast(img.pf, C.POINTER(pt._abi.Float3)), C.cast(img.pu, C.POINTER(pt._abi.UChar3)), p,
+                               C.byref(cam), v.sky_cube_map, *scratch, v.mesh_textures, C.byref(cfg))
+        oracle.render(v, cam, cfg, p, 1, image=want, image256=want8)
+
+    def cpu(p):
+        assert hip.hipDeviceSynchronize() == 0
+        f, u = img.host_arrays()
+        for im, im8 in ((f, u), (want, want8)):
+            oracle.render(v, cam, cfg, p, 1, rng="msvc", math="libm", arith="plain", image=im, image256=im8)
+
+    try:
+        gpu(1)
+        gpu(2)
+        if edit:  # the knot's material (every knot triangle points at it), edited in place
+            m = v.triangles[v.triangle_num - 1].mat.contents
+            m.diffuse_color.x = float(np.float32(0.25))
+            m.diffuse_color.z = float(np.float32(0.9))
+        cpu(1)
+        cpu(2)
+        gpu(3)
+        got, got8 = img.read()
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), \
+            f"{(got != want).any(axis=1).sum()} / {n} pixels differ (float)"
+        assert np.array_equal(got8, want8)
+        gpu(4)  # and the library's own continuation after the redo
+        got, got8 = img.read()
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+        assert np.array_equal(got8, want8)
+    finally:
+        lib.path_tracer_kernel_memory_free(*scratch)
+        img.free()

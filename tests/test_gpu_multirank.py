@@ -116,3 +116,25 @@ def test_frame_groups_on_hip_equal_the_oracle(require_gpu, tmp_path, ranks, coll
             img8 = np.load(f"{out}_{k}_{j}_u8.npy")
             assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), f"context {k} frame {j}: float"
             assert np.array_equal(img8, ref8), f"context {k} frame {j}: 8-bit"
+
+
+def test_rank0_continues_accumulating_after_gather8_groups(require_gpu, tmp_path):
+    """gather8 (bench.py's tiled default) moves only the 8-bit rows per group, leaving each rank's float running sums on
+    that rank. A caller that keeps accumulating on rank 0 — continuation passes add into the running sum
+    (Core/path_tracer.cpp:40-67, path_tracer_kernel.cu:644-651) — first calls collect_float(); rank 0's sum then
+    continues to the oracle's 2 SPP-pass sum bit for bit, over every row, its own and the other ranks'."""
+    out = str(tmp_path / "cont")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(HERE, "gpu_multirank_worker.py"), out, "gather8", "3", "2", "3", "continue"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert res.returncode == 0, res.stderr[-4000:]
+    sc = worker.scene()
+    cfg = pt.configuration(max_tracer_depth=8)
+    cam = pt.camera(worker.W, worker.H, yaw=0.0, **worker.CAM)
+    ref, ref8, _ = oracle.render(sc.view, cam, cfg, 1, 2 * worker.SPP)
+    img = np.load(f"{out}_cont_f.npy")
+    img8 = np.load(f"{out}_cont_u8.npy")
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), f"{(img != ref).any(axis=1).sum()} pixels differ"
+    assert np.array_equal(img8, ref8)

@@ -224,3 +224,63 @@ def test_two_rank_tiled_frame_equals_single_render(tmp_path, world, collective, 
     # the ranks' bands are disjoint and cover the frame (non-root buffers are scratch after the collective)
     owned = np.concatenate([r["owned"] for r in rs])
     assert np.array_equal(np.sort(owned), np.arange(W * H))
+
+
+def _stage_run(tmp_path, world, stall, limit):
+    import subprocess
+    import sys
+    import time
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(here, "dist_stage_worker.py"), str(tmp_path / "st"), str(stall), str(limit)]
+    t0 = time.monotonic()
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
+                         env=dict(os.environ, OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1"))
+    return res, time.monotonic() - t0
+
+
+@pytest.mark.timeout(300)
+def test_stalled_rank_fails_the_job_within_the_stage_limit(tmp_path):
+    """bench.py's fail-fast path (init_distributed's collective timeout + pt.StageWatch) over gloo: rank 1's renderer
+    hangs before its group's gather; the job must exit non-zero well before its outer limit, with a stderr line naming
+    a rank and the stage it was stuck in (rank 1 in its render, rank 0 in the gather: both are 'timed run')."""
+    res, took = _stage_run(tmp_path, 2, 1, 6)
+    assert res.returncode != 0, res.stderr[-3000:]
+    assert took < 120, took
+    assert "stage 'timed run' did not finish within 6 s" in res.stderr, res.stderr[-3000:]
+    assert "rank 1: stage" in res.stderr or "rank 0: stage" in res.stderr, res.stderr[-3000:]
+    assert not (tmp_path / "st_breakdown.json").exists()
+
+
+@pytest.mark.timeout(300)
+def test_rank_breakdown_reports_every_rank(tmp_path):
+    """The same job without a stall: rank_breakdown (bench.py's config.per_rank) lists both ranks' render and
+    collective time per launch over the two timed launches."""
+    import json
+
+    res, _ = _stage_run(tmp_path, 2, -1, 120)
+    assert res.returncode == 0, res.stderr[-3000:]
+    bd = json.load(open(tmp_path / "st_breakdown.json"))
+    assert bd["launches_timed_per_rank"] == [2, 2], bd
+    assert len(bd["render_ms_per_launch"]) == 2 and min(bd["render_ms_per_launch"]) > 0, bd
+    assert len(bd["collective_ms_per_launch"]) == 2 and min(bd["collective_ms_per_launch"]) >= 0, bd
+    assert bd["render_ms_per_launch_max_over_ranks"] == max(bd["render_ms_per_launch"]), bd
+
+
+def test_stage_watch_names_the_stage_and_exits():
+    """pt.StageWatch alone: a stage that outlives its limit ends the process with exit code 124 and one stderr line;
+    a stage left in time does not."""
+    import subprocess
+    import sys
+
+    code = ("import time, pathtracerwithcuda_amd as pt\n"
+            "w = pt.StageWatch(3, 1.0)\n"
+            "w.stage('quick'); time.sleep(0.3)\n"
+            "w.stage('stuck gather'); time.sleep(30)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, cwd=root)
+    assert res.returncode == 124, (res.returncode, res.stderr)
+    assert "[bench] rank 3: stage 'stuck gather' did not finish within 1 s" in res.stderr, res.stderr
+    assert "quick" not in res.stderr
