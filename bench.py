@@ -117,14 +117,20 @@ class Workload:
     diffuse-only mesh, no spheres); c3-c5 are the heavier BASELINE.json configs
     (1 GPU or tiled), for one-off measurements of the same path at their sizes."""
 
-    def __init__(self, name: str):
+    # BVH builders a workload can be built with: the reference's Morton LBVH (its config default MortonCodeCUDA,
+    # Bvh/bvh.cpp:862-1047) and PT_BVH_SAH, the surface-area tree (a stated-tolerance mode, DESIGN.md §5)
+    TREES = {"lbvh": 2, "sah": 3}
+
+    def __init__(self, name: str, tree: str = "lbvh", leaf: int = 1):
         import pathtracerwithcuda_amd as pt
 
         self.name = name
+        self.tree, self.leaf = tree, leaf  # leaf: BvhLeafNodeTriangleNum (the reference's config: 1)
+        method = self.TREES[tree]
         cam_kw = dict(CAMERA)
         if name == "metric":
             self.width, self.height, self.spp, self.depth = WIDTH, HEIGHT, SPP, DEPTH
-            self.scene = pt.cornell_scene(pt.torus_knot(*KNOT))
+            self.scene = pt.cornell_scene(pt.torus_knot(*KNOT), method=method, leaf_size=leaf)
             self.key = f"cornell+knot{KNOT[0] * KNOT[1] * 2}_{WIDTH}x{HEIGHT}_spp{SPP}_d{DEPTH}"
             self.desc = ("Cornell box (cornell.obj walls, cube.obj light, iron+glass spheres) + torus knot, "
                          f"{self.scene.triangle_count} triangles, {self.scene.view.sphere_num} spheres")
@@ -139,7 +145,8 @@ class Workload:
             self.data = "synthetic: spheres-only Cornell box (cornell_box_simple.json materials) + procedural 512^2 cube map"
         elif name == "c2":  # Cornell + ~70k-triangle mesh, diffuse only, 1280x720
             self.width, self.height, self.spp, self.depth = 1280, 720, 8, 8
-            self.scene = pt.cornell_scene(pt.torus_knot(*KNOT), mesh_material="diffuse_white", spheres=False)
+            self.scene = pt.cornell_scene(pt.torus_knot(*KNOT), mesh_material="diffuse_white", spheres=False,
+                                          method=method, leaf_size=leaf)
             self.key = f"c2_cornell+knot{KNOT[0] * KNOT[1] * 2}_diffuse_1280x720_spp8_d8"
             self.desc = ("Cornell box (cornell.obj walls, cube.obj light) + torus knot, diffuse only (specular 0, "
                          f"n = 1.000293), no spheres, {self.scene.triangle_count} triangles")
@@ -154,14 +161,15 @@ class Workload:
             sc.add_mesh([pt.cube_shape()], [sc.add_material("light")], position=(0.0, 3.1, 0.0),
                         scale=(0.85, 0.05, 0.85))
             sc.set_cube_map(pt.procedural_cube_map(512))
-            self.scene = sc.build()
+            self.scene = sc.build(leaf_size=leaf, method=method)
             cam_kw.update(aperture=0.1, focal=12.5)
             self.key = "c3_microfacet_sky_dof_1920x1080_spp64_d8"
             self.desc = "six GGX spheres (roughness 0.01..1, silver n=0.04 k=2.65), Cornell walls + light, skybox, DoF 0.1"
             self.data = "synthetic: micro_surface.json spheres + procedural 512^2 cube map"
         elif name == "c4":  # ~800k-triangle mesh with the dragon's subsurface material
             self.width, self.height, self.spp, self.depth = 1920, 1080, 256, 8
-            self.scene = pt.cornell_scene(pt.torus_knot(1000, 400), mesh_material="DragonGreen")
+            self.scene = pt.cornell_scene(pt.torus_knot(1000, 400), mesh_material="DragonGreen", method=method,
+                                          leaf_size=leaf)
             self.key = "c4_knot800000_sss_1920x1080_spp256_d8"
             self.desc = (f"Cornell box + {self.scene.triangle_count - 22}-triangle torus knot (dragon stand-in) "
                          "with DragonGreen subsurface scattering (sigma_a (40,3,14), sigma_s' 400)")
@@ -174,7 +182,7 @@ class Workload:
             # *_spec.tga specular maps (512^2 RGBA, 512^2 RGB, 1024^2 RGB), in the Cornell walls under the
             # cube light, lobby skybox
             root = asset_root()
-            cfg = pt.configuration(max_tracer_depth=self.depth)
+            cfg = pt.configuration(max_tracer_depth=self.depth, bvh_build=method, bvh_leaf_node_triangle_num=leaf)
             self.scene = pt.load_scene(os.path.join(root, "res", "scene", "c5_vanille_gallery.json"), root_dir=root,
                                        config=cfg)
             cam_kw = dict(pitch=0.1, radius=9.0, center=(0.0, 0.9, 0.0))  # the room's front opening
@@ -184,7 +192,7 @@ class Workload:
             self.data = "the reference's own meshes, TGA maps and lobby skybox (tests/golden/ref_assets.tar.xz)"
         else:
             raise SystemExit(f"unknown workload {name!r}")
-        self.cfg = pt.configuration(max_tracer_depth=self.depth)
+        self.cfg = pt.configuration(max_tracer_depth=self.depth, bvh_leaf_node_triangle_num=leaf)
         self.cam_kw = cam_kw
         self.cam = pt.camera(self.width, self.height, **cam_kw)
 
@@ -306,6 +314,12 @@ def main() -> int:
     ap.add_argument("--workload", choices=["metric", "c1", "c2", "c3", "c4", "c5"], default="metric",
                     help="metric: BASELINE.json's metric configuration (default); c1: its CPU-path plumbing config "
                          "(the line then carries that frame's CPU-path time as cpu_baseline); c2-c5: its other configs")
+    ap.add_argument("--tree", choices=list(Workload.TREES), default=os.environ.get("PT_BENCH_TREE", "lbvh"),
+                    help="the BVH the timed frames walk: lbvh, the reference's Morton LBVH (Bvh/bvh.cpp:862-1047, its "
+                         "config default), or sah, PT_BVH_SAH (DESIGN.md §5)")
+    ap.add_argument("--no-alt-tree", action="store_true",
+                    help="at N = 1 the line also times the other tree on the same frames (config.alt_tree) and checks "
+                         "that both render the same image; this skips both")
     ap.add_argument("--orbit", type=float, default=0.0, metavar="RAD",
                     help="advance the camera's yaw by RAD per frame (an interactive caller's moving camera); every "
                          "frame then has its own camera, 0 (default) keeps one camera for all frames")
@@ -397,7 +411,7 @@ def main() -> int:
     # whose tails are a small part of them.
     # Nor for frames of more than one pass launch (C3's 64 passes: 25107 vs 25870 Mrays/s with 8 per launch):
     # their launches already follow each other on a context.
-    wl = Workload(args.workload)
+    wl = Workload(args.workload, tree=args.tree)
     # At 8 waves (profiles/r04/group/group_size_n2_n4.txt) 8 per launch beats 4 at N = 2 too (2.595-2.605 vs
     # 2.653-2.659 ms per frame). The tail is paid per launch and lasts about 1 ms whatever the share (the last
     # paths in flight), so a rank's launch carries 8 whole frames' units at every N: G = 8 N frames of a 1/N
@@ -559,6 +573,48 @@ def main() -> int:
     latency = (time.perf_counter() - t1) / max(lat_frames, 1)
     solo_ms, solo_launches = r.kernel_time_kind(kind)
 
+    # The other tree on the same frames (N = 1): the reference's LBVH beside PT_BVH_SAH, or the other way round, timed
+    # the same way (warm-up, K timed frames, one-frame-in-flight launches for the roofline), and one frame of each
+    # compared bit for bit (the trees' closest hits differ only where the walk order decides them)
+    alt = None
+    if world == 1 and not distributed and not args.no_alt_tree:
+        alt_tree = "lbvh" if args.tree == "sah" else "sah"
+        awl = Workload(args.workload, tree=alt_tree)
+        for q in rs:
+            q.synchronize()
+            q.upload(awl.scene, cfg)
+        run(args.warmup)
+        torch.cuda.synchronize()
+        for q in rs:
+            q.stats_reset()
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        run(args.steps)
+        torch.cuda.synchronize()
+        a_elapsed = time.perf_counter() - ta
+        a_segments = sum(q.stats()["segments"] for q in rs)
+        r.set_grid_share(100)
+        r.stats_reset()
+        for _ in range(lat_frames):
+            frames[0].render(cam, cfg, spp)
+        a_ms, a_n = r.kernel_time_kind(kind)
+        chk = pt.Renderer(local)
+        try:
+            chk.set_schedule(args.schedule)
+            imgs = []
+            for sc_ in (wl.scene, awl.scene):
+                chk.upload(sc_, cfg)
+                chk.setup_frame(width, height)
+                chk.render(cam, cfg, 1, spp, write_u8=2)
+                imgs.append(chk.download())
+        finally:
+            chk.close()
+        (f0, u0), (f1, u1) = imgs
+        differ = int((f0.view(np.uint32) != f1.view(np.uint32)).any(axis=-1).sum())
+        alt = {"tree": alt_tree, "scene": awl.scene, "elapsed": a_elapsed, "segments": a_segments,
+               "avg_launch_s": a_ms / max(a_n, 1) / 1000.0, "pixels_differ": differ,
+               "pixels_differ_u8": int((u0 != u1).any(axis=-1).sum()), "key": awl.key}
+
     if distributed:
         watch.stage("max over ranks")
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
@@ -603,7 +659,9 @@ def main() -> int:
         bytes_per_launch = extend_bytes(counts, scene.view.sphere_num) / world / frame_launches
         kernel_name = "extend_kernel<LEAF1=true,STATS=false>"
     workload = wl.key
-    key = workload + ("" if schedule == "persistent" else "/wavefront") + ("/medium_bound" if args.medium_bound else "")
+    # profiles/traffic.json keys: the workload, then "/sah" for the PT_BVH_SAH tree (the reference tree unsuffixed)
+    suffix = ("" if schedule == "persistent" else "/wavefront") + ("/medium_bound" if args.medium_bound else "")
+    key = workload + ("/sah" if args.tree == "sah" else "") + suffix
     # N > 1: rank 0's share profiled on its own (tools/gpu_share_pmc.sh, "<key>/tiled<N>"); otherwise the
     # whole 1-GPU frame's profile, of which a rank of N runs 1/N
     prof = load_profile(f"{key}/tiled{world}") if world > 1 else {}
@@ -713,6 +771,27 @@ def main() -> int:
     rf = line["roofline"]
     if hbm is not None and (valu["frac"] is None or hbm["frac"] > valu["frac"]):
         rf.update(bound="hbm", achieved=hbm["achieved"], peak=hbm["peak"], unit=hbm["unit"], frac=hbm["frac"])
+    line["config"]["tree"] = args.tree
+    if alt is not None:
+        aprof = load_profile(alt["key"] + ("/sah" if alt["tree"] == "sah" else "") + suffix)
+        a_valu = aprof.get("valu_insts_per_launch")
+        a_hbm = aprof.get("hbm_bytes_per_launch")
+        a_vf = float(a_valu) / alt["avg_launch_s"] / 1e9 / valu_peak if a_valu else None
+        a_hf = float(a_hbm) / alt["avg_launch_s"] / 1e9 / HBM_PEAK_GBS if a_hbm else None
+        a_bound = "hbm" if (a_hf is not None and (a_vf is None or a_hf > a_vf)) else "valu"
+        line["config"]["alt_tree"] = {
+            "tree": alt["tree"],
+            "value": round(alt["segments"] / alt["elapsed"] / 1e6, 3),
+            "ms_per_step": round(alt["elapsed"] / args.steps * 1000.0, 3),
+            "avg_launch_ms": round(alt["avg_launch_s"] * 1000.0, 4),
+            "roofline": {"bound": a_bound, "frac": round(a_hf if a_bound == "hbm" else a_vf, 4) if (a_vf or a_hf) else None,
+                         "valu_frac": round(a_vf, 4) if a_vf else None, "hbm_frac": round(a_hf, 4) if a_hf else None,
+                         "valu_insts_per_launch": a_valu, "hbm_bytes_per_launch": a_hbm},
+            "segments_per_frame": alt["segments"] // max(args.steps, 1),
+            # one frame of each tree through the same camera, compared bit for bit
+            "image_pixels_differ": alt["pixels_differ"], "image_pixels_differ_u8": alt["pixels_differ_u8"],
+        }
+        line["config"]["image_matches_reference_tree"] = alt["pixels_differ"] == 0 and alt["pixels_differ_u8"] == 0
     if distributed:
         line["config"]["image_matches_1gpu"] = matches_1gpu
         line["config"]["collective"] = {"backend": dist.get_backend(), "world_size": world,

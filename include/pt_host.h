@@ -38,6 +38,14 @@ int pt_bvh_build_ex(const pt_triangle* triangles, int n, int start_index, int le
                     pt_bvh_node_device** nodes, int* node_num, int** leaf_indices, int* leaf_num);
 int pt_bvh_build_naive(const pt_triangle* triangles, int n, int start_index, int leaf_size, int bucket_num,
                        pt_bvh_node_device** nodes, int* node_num, int** leaf_indices, int* leaf_num);
+/* PT_BVH_SAH (not a reference builder): centroids binned into `bins` bins per axis, splits priced by true surface
+ * area, leaves of at most leaf_size triangles, then the reference's preorder flattening. Same output contract. */
+int pt_bvh_build_sah(const pt_triangle* triangles, int n, int start_index, int leaf_size, int bins,
+                     pt_bvh_node_device** nodes_out, int* node_num_out, int** leaf_indices_out, int* leaf_num_out);
+/* The same tree built on the HIP device (pt_bvh_sah.hip: one launch per tree level, one workgroup per node), flattened
+ * on the host; node arrays byte-equal to pt_bvh_build_sah's. bins 2..64. Returns -3 on a HIP error. */
+int pt_bvh_build_sah_device(const pt_triangle* triangles, int n, int start_index, int leaf_size, int bins,
+                            pt_bvh_node_device** nodes_out, int* node_num_out, int** leaf_indices_out, int* leaf_num_out);
 
 /* Morton helpers exposed for known-answer tests (Bvh/bvh.cpp:370-441). */
 unsigned int pt_morton_code(float x, float y, float z);

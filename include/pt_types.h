@@ -127,7 +127,11 @@ typedef struct pt_render_camera {
 enum pt_bvh_build_method {
     PT_BVH_NAIVE_CPU = 0,
     PT_BVH_MORTON_CODE_CPU = 1,
-    PT_BVH_MORTON_CODE_CUDA = 2
+    PT_BVH_MORTON_CODE_CUDA = 2,
+    /* not a reference method: a binned true-surface-area tree (pt_bvh_build_sah; its GPU twin pt_bvh_build_sah_device),
+     * flattened like the others; the closest hit may differ from the reference tree's where visit order decides it
+     * (ties, grazed boxes): a stated-tolerance mode, DESIGN.md §5 */
+    PT_BVH_SAH = 3
 };
 
 /* Core/configuration.h:9-34 */

@@ -253,6 +253,10 @@ _PROTOS = {
                                   C.POINTER(C.POINTER(BvhNodeDevice)), c_int_p, C.POINTER(c_int_p), c_int_p]),
     "pt_bvh_build_naive": (C.c_int, [C.POINTER(Triangle), C.c_int, C.c_int, C.c_int, C.c_int,
                                      C.POINTER(C.POINTER(BvhNodeDevice)), c_int_p, C.POINTER(c_int_p), c_int_p]),
+    "pt_bvh_build_sah": (C.c_int, [C.POINTER(Triangle), C.c_int, C.c_int, C.c_int, C.c_int,
+                                   C.POINTER(C.POINTER(BvhNodeDevice)), c_int_p, C.POINTER(c_int_p), c_int_p]),
+    "pt_bvh_build_sah_device": (C.c_int, [C.POINTER(Triangle), C.c_int, C.c_int, C.c_int, C.c_int,
+                                          C.POINTER(C.POINTER(BvhNodeDevice)), c_int_p, C.POINTER(c_int_p), c_int_p]),
     "pt_scene_builder_build_ex": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
     "pt_scene_builder_set_bvh_device": (C.c_int, [C.c_void_p, C.c_int]),
     # GPU BVH builder (include/pt_bvh.h)

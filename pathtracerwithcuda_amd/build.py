@@ -29,7 +29,7 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "
 # It does not change a single rounding (no contraction, no reassociation): parity stays bit-exact.
 HIP_FLAGS = ["-fno-slp-vectorize"] + os.environ.get("PT_EXTRA_FLAGS", "").split()
 
-HIP_SOURCES = ["pt_kernels.hip", "pt_wavefront.hip", "pt_bvh.hip", "pt_runtime.cpp"]
+HIP_SOURCES = ["pt_kernels.hip", "pt_wavefront.hip", "pt_bvh.hip", "pt_bvh_sah.hip", "pt_runtime.cpp"]
 CXX_SOURCES = ["pt_host.cpp", "pt_loader.cpp", "pt_image.cpp", "pt_jpeg.cpp"]
 LINK_LIBS = ["-lz"]  # zlib: PNG inflate/deflate (pt_image.cpp)
 

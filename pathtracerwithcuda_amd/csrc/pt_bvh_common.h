@@ -43,6 +43,15 @@ PT_HD inline void expand(Box& a, const Box& b) {
     }
 }
 
+// -0 -> +0 in every coordinate (x + 0.0f): PT_BVH_SAH's boxes, so that unions are the same in any order (the
+// reference's a < b ? a : b keeps whichever of two zeros came last); no slab-test outcome depends on a zero's sign
+PT_HD inline void canonical_zeros(Box& b) {
+    for (int k = 0; k < 3; k++) {
+        b.lb[k] = b.lb[k] + 0.0f;
+        b.rt[k] = b.rt[k] + 0.0f;
+    }
+}
+
 PT_HD inline bool is_thin(const Box& b) {  // bounding_box::is_thin_bounding_box
     return b.rt[0] == b.lb[0] || b.rt[1] == b.lb[1] || b.rt[2] == b.lb[2];
 }

@@ -30,3 +30,17 @@ inline unsigned int pt_leaf_count(int n, int leaf_size) {
 // Bottom-up boxes and the flattened skip-pointer array (Bvh/bvh.cpp:974-1047, :244-330).
 int pt_morton_finish(PtMortonTree& t, int leaf_size, pt_bvh_node_device** nodes_out, int* node_num_out,
                      int** leaf_out, int* leaf_num_out);
+
+// A linked tree (bvh_naive_cpu's build nodes, PT_BVH_SAH's, host or device): node 0 is the root; a leaf holds
+// leaf_size triangle ids (-1 padded).
+struct PtTreeNode {
+    ptbvh::Box box;
+    int left = -1, right = -1, parent = -1;
+    bool leaf = false;
+    std::vector<int> tris;
+};
+
+// build_bvh_device_data (Bvh/bvh.cpp:244-330) over a linked tree: preorder, skip indices, thin leaf boxes widened to
+// the parent's (pt_host.cpp).
+int pt_flatten_tree(std::vector<PtTreeNode>& nodes, int leaf_size, pt_bvh_node_device** nodes_out, int* node_num_out,
+                    int** leaf_out, int* leaf_num_out);

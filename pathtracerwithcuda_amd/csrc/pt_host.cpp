@@ -233,12 +233,7 @@ extern "C" void pt_bvh_free(pt_bvh_node_device* nodes, int* leaf_indices) {
 // ---- bvh_naive_cpu (Bvh/bvh.cpp:16-330): bucketed "SAH" split, then the same preorder flattening --
 namespace {
 
-struct GNode {
-    Box box;
-    int left = -1, right = -1, parent = -1;
-    bool leaf = false;
-    std::vector<int> tris;
-};
+using GNode = PtTreeNode;
 
 inline float centroid_axis(const Box& b, int axis) { return 0.5f * (b.rt[axis] + b.lb[axis]); }
 inline void box_of_box(Box& dst, const Box& src) { dst = src; }
@@ -397,6 +392,11 @@ int flatten_tree(std::vector<GNode>& nodes, int leaf_size, pt_bvh_node_device** 
 
 }  // namespace
 
+int pt_flatten_tree(std::vector<PtTreeNode>& nodes, int leaf_size, pt_bvh_node_device** nodes_out, int* node_num_out,
+                    int** leaf_out, int* leaf_num_out) {
+    return flatten_tree(nodes, leaf_size, nodes_out, node_num_out, leaf_out, leaf_num_out);
+}
+
 // bvh_naive_cpu::build_bvh (Bvh/bvh.cpp:185-219) + build_bvh_device_data (:244-330).
 extern "C" int pt_bvh_build_naive(const pt_triangle* tris, int n, int start_index, int leaf_size, int bucket_num,
                                   pt_bvh_node_device** nodes_out, int* node_num_out, int** leaf_out, int* leaf_num_out) {
@@ -419,10 +419,153 @@ extern "C" int pt_bvh_build_naive(const pt_triangle* tris, int n, int start_inde
     return flatten_tree(nodes, leaf_size, nodes_out, node_num_out, leaf_out, leaf_num_out);
 }
 
+// ---- PT_BVH_SAH: a binned surface-area-heuristic tree (not a reference builder) ------------------------------------
+// The reference's trees are its Morton LBVH (config default MortonCodeCUDA, Bvh/bvh.cpp:862-1047) and a bucketed
+// split priced by 2 * VOLUME (bounding_box.h:63-66, bvh.cpp:117). This one prices splits by true surface area
+// (MacDonald & Booth): per node, the triangle centroids binned along each axis (`bins` equal bins over the centroid
+// extent), the split minimising SA(left) * n(left) + SA(right) * n(right), leaves of at most `leaf_size` triangles
+// (one triangle per leaf at the reference's BvhLeafNodeTriangleNum = 1). The tree is flattened exactly as the
+// reference flattens its own (flatten_tree: preorder, skip indices, thin leaf boxes widened to the parent's), so the
+// walk (path_tracer_kernel.cu:111-150) and every kernel run on it unchanged; the closest hit differs from the
+// reference tree's only where the walk order decides it (ties, boxes grazed in float), DESIGN.md §5.
+// Preorder child order (PT_SAH_ORDER, the study's knob): 0 the lower side of the split first, 1 the child of larger
+// surface area first, 2 (default) the child with more triangles first: on whole frames 2 walks the fewest nodes
+// (metric -8.0 %, C4 -13.5 % against the reference tree; 0: -6.5 %, -11.0 %; profiles/r06/tree/).
+namespace {
+
+inline double sa_of(const Box& b) {
+    const double x = (double)b.rt[0] - b.lb[0], y = (double)b.rt[1] - b.lb[1], z = (double)b.rt[2] - b.lb[2];
+    return 2.0 * (x * y + y * z + z * x);
+}
+
+int sah_build(const pt_triangle* tris, int n, int start, int leaf_size, int bins, std::vector<GNode>& nodes) {
+    const char* order_env = std::getenv("PT_SAH_ORDER");
+    const int order = order_env ? std::atoi(order_env) : 2;
+    bins = std::max(2, std::min(bins, 256));
+    std::vector<Box> box((size_t)n);
+    std::vector<float> cen((size_t)n * 3);
+    for (int i = 0; i < n; i++) {
+        box[(size_t)i] = box_of_triangle(tris[i]);
+        ptbvh::canonical_zeros(box[(size_t)i]);  // the device builder's unions are order-free (pt_bvh_sah.hip)
+        for (int k = 0; k < 3; k++) cen[(size_t)i * 3 + k] = 0.5f * (box[(size_t)i].lb[k] + box[(size_t)i].rt[k]);
+    }
+    std::vector<int> idx((size_t)n);
+    for (int i = 0; i < n; i++) idx[(size_t)i] = i;
+    struct Task { int node, begin, end; };
+    nodes.assign(1, GNode{});
+    std::vector<Task> stack{{0, 0, n}};
+    std::vector<Box> bbox((size_t)bins);
+    std::vector<int> bcnt((size_t)bins);
+    std::vector<char> binit((size_t)bins);
+    std::vector<double> right_sa((size_t)bins);
+    std::vector<int> right_n((size_t)bins);
+    while (!stack.empty()) {
+        const Task t = stack.back();
+        stack.pop_back();
+        const int cnt = t.end - t.begin;
+        Box nb = box[(size_t)idx[(size_t)t.begin]];
+        float clo[3], chi[3];
+        for (int k = 0; k < 3; k++) clo[k] = chi[k] = cen[(size_t)idx[(size_t)t.begin] * 3 + k];
+        for (int i = t.begin + 1; i < t.end; i++) {
+            const int j = idx[(size_t)i];
+            expand(nb, box[(size_t)j]);
+            for (int k = 0; k < 3; k++) {
+                clo[k] = std::min(clo[k], cen[(size_t)j * 3 + k]);
+                chi[k] = std::max(chi[k], cen[(size_t)j * 3 + k]);
+            }
+        }
+        nodes[(size_t)t.node].box = nb;
+        if (cnt <= leaf_size) {
+            GNode& g = nodes[(size_t)t.node];
+            g.leaf = true;
+            g.tris.assign((size_t)leaf_size, -1);
+            for (int i = 0; i < cnt; i++) g.tris[(size_t)i] = idx[(size_t)(t.begin + i)] + start;
+            continue;
+        }
+        double best = INFINITY;
+        int best_axis = -1, best_bin = 0;
+        for (int k = 0; k < 3; k++) {
+            const float ext = chi[k] - clo[k];
+            if (!(ext > 0.0f)) continue;
+            const float scale = (float)bins / ext;
+            std::fill(bcnt.begin(), bcnt.end(), 0);
+            std::fill(binit.begin(), binit.end(), 0);
+            for (int i = t.begin; i < t.end; i++) {
+                const int j = idx[(size_t)i];
+                const int b = std::min(bins - 1, (int)((cen[(size_t)j * 3 + k] - clo[k]) * scale));
+                if (!binit[(size_t)b]) { bbox[(size_t)b] = box[(size_t)j]; binit[(size_t)b] = 1; }
+                else expand(bbox[(size_t)b], box[(size_t)j]);
+                bcnt[(size_t)b]++;
+            }
+            Box acc{};
+            bool any = false;
+            int nr = 0;
+            for (int b = bins - 1; b >= 1; b--) {  // right side = bins [b, bins)
+                if (binit[(size_t)b]) { if (!any) { acc = bbox[(size_t)b]; any = true; } else expand(acc, bbox[(size_t)b]); }
+                nr += bcnt[(size_t)b];
+                right_sa[(size_t)b] = any ? sa_of(acc) : 0.0;
+                right_n[(size_t)b] = nr;
+            }
+            any = false;
+            int nl = 0;
+            for (int b = 1; b < bins; b++) {  // left side = bins [0, b)
+                if (binit[(size_t)(b - 1)]) {
+                    if (!any) { acc = bbox[(size_t)(b - 1)]; any = true; } else expand(acc, bbox[(size_t)(b - 1)]);
+                }
+                nl += bcnt[(size_t)(b - 1)];
+                if (nl == 0 || right_n[(size_t)b] == 0) continue;
+                const double c = sa_of(acc) * nl + right_sa[(size_t)b] * right_n[(size_t)b];
+                if (c < best) { best = c; best_axis = k; best_bin = b; }
+            }
+        }
+        int mid;
+        if (best_axis < 0) {  // every centroid the same: split the range in half
+            mid = t.begin + cnt / 2;
+        } else {
+            const float scale = (float)bins / (chi[best_axis] - clo[best_axis]);
+            const auto it = std::stable_partition(idx.begin() + t.begin, idx.begin() + t.end, [&](int j) {
+                return std::min(bins - 1, (int)((cen[(size_t)j * 3 + best_axis] - clo[best_axis]) * scale)) < best_bin;
+            });
+            mid = (int)(it - idx.begin());
+        }
+        const int l = (int)nodes.size(), r = l + 1;
+        nodes.emplace_back();
+        nodes.emplace_back();
+        nodes[(size_t)l].parent = nodes[(size_t)r].parent = t.node;
+        int first = l, second = r;  // preorder: `first` is walked first
+        if (order != 0) {
+            Box bl = box[(size_t)idx[(size_t)t.begin]], br = box[(size_t)idx[(size_t)mid]];
+            for (int i = t.begin + 1; i < mid; i++) expand(bl, box[(size_t)idx[(size_t)i]]);
+            for (int i = mid + 1; i < t.end; i++) expand(br, box[(size_t)idx[(size_t)i]]);
+            const bool swap = order == 1 ? sa_of(br) > sa_of(bl) : (t.end - mid) > (mid - t.begin);
+            if (swap) std::swap(first, second);
+        }
+        nodes[(size_t)t.node].left = first;
+        nodes[(size_t)t.node].right = second;
+        stack.push_back({r, mid, t.end});
+        stack.push_back({l, t.begin, mid});
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int pt_bvh_build_sah(const pt_triangle* tris, int n, int start_index, int leaf_size, int bins,
+                                pt_bvh_node_device** nodes_out, int* node_num_out, int** leaf_out, int* leaf_num_out) {
+    if (!tris || n <= 0 || leaf_size <= 0 || bins <= 0 || !nodes_out || !node_num_out || !leaf_out || !leaf_num_out)
+        return -1;
+    std::vector<GNode> nodes;
+    int rc = sah_build(tris, n, start_index, leaf_size, bins, nodes);
+    if (rc != 0) return rc;
+    return flatten_tree(nodes, leaf_size, nodes_out, node_num_out, leaf_out, leaf_num_out);
+}
+
 extern "C" int pt_bvh_build_ex(const pt_triangle* tris, int n, int start_index, int leaf_size, int method, int bucket_num,
                                pt_bvh_node_device** nodes_out, int* node_num_out, int** leaf_out, int* leaf_num_out) {
     if (method == PT_BVH_NAIVE_CPU)
         return pt_bvh_build_naive(tris, n, start_index, leaf_size, bucket_num, nodes_out, node_num_out, leaf_out, leaf_num_out);
+    if (method == PT_BVH_SAH)
+        return pt_bvh_build_sah(tris, n, start_index, leaf_size, 32, nodes_out, node_num_out, leaf_out, leaf_num_out);
     // MortonCodeCPU and MortonCodeCUDA build the same tree (Bvh/bvh.cpp:667-780 vs :862-1047); the
     // CPU variant's std::sort is not stable, so equal codes keep their input order here as in the
     // CUDA variant's merge sort.
@@ -614,12 +757,16 @@ namespace {
 int build_mesh_bvh(pt_scene_builder* b, size_t m, pt_bvh_node_device** nodes, int* nn, int** leaf, int* ln) {
     // MortonCodeCUDA runs on the GPU (pt_bvh.hip); its node array equals the host builder's bit for bit
     // (tests/test_bvh_device.py), which therefore serves machines without a HIP device
-    const bool on_device = b->build_method == PT_BVH_MORTON_CODE_CUDA &&
-                           (b->bvh_device >= 0 || (b->bvh_device == -2 && pt_device_count() > 0));
-    return on_device ? pt_bvh_build_device(b->triangles.data() + b->mesh_start[m], b->mesh_count[m], b->mesh_start[m],
-                                           b->build_leaf, nodes, nn, leaf, ln)
-                     : pt_bvh_build_ex(b->triangles.data() + b->mesh_start[m], b->mesh_count[m], b->mesh_start[m],
-                                       b->build_leaf, b->build_method, b->build_bucket, nodes, nn, leaf, ln);
+    // PT_BVH_SAH likewise (pt_bvh_sah.hip, the host builder's tree byte for byte) for meshes large enough to pay for
+    // the launches
+    const bool device = b->bvh_device >= 0 || (b->bvh_device == -2 && pt_device_count() > 0);
+    const pt_triangle* t = b->triangles.data() + b->mesh_start[m];
+    if (device && b->build_method == PT_BVH_MORTON_CODE_CUDA)
+        return pt_bvh_build_device(t, b->mesh_count[m], b->mesh_start[m], b->build_leaf, nodes, nn, leaf, ln);
+    if (device && b->build_method == PT_BVH_SAH && b->mesh_count[m] >= 4096)
+        return pt_bvh_build_sah_device(t, b->mesh_count[m], b->mesh_start[m], b->build_leaf, 32, nodes, nn, leaf, ln);
+    return pt_bvh_build_ex(t, b->mesh_count[m], b->mesh_start[m], b->build_leaf, b->build_method, b->build_bucket,
+                           nodes, nn, leaf, ln);
 }
 
 // The boxes of a fresh build are the mesh's initial boxes, under its current transform

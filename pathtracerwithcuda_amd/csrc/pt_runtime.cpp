@@ -1136,21 +1136,6 @@ int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, con
     if (prc != PT_OK) return prc;
     for (int f = 1; f < frames; f++)
         if ((int)cams[f].resolution.x != ctx->width) { set_error("camera width != frame width"); return PT_E_ARG; }
-    // every frame's accumulate runs at once (accumulate_frames_kernel, blockIdx.y = frame): the frames' buffers must
-    // not alias one another
-    {
-        std::vector<const void*> seen;
-        seen.reserve((size_t)frames * 2);
-        for (int f = 0; f < frames; f++) {
-            seen.push_back(images[f]);
-            if (images256 && images256[f]) seen.push_back(images256[f]);
-        }
-        std::sort(seen.begin(), seen.end());
-        if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) {
-            set_error("pt_render_frames: two frames share an image buffer");
-            return PT_E_ARG;
-        }
-    }
     const int feat = render_feat(ctx, lp.cfg);
     PassChoice pc = pass_choice(ctx, feat);
     const bool fused = frames > 1 && !wavefront_schedule(ctx) && pass_uses_unified(pc, pass_lds_bytes(ctx)) &&
@@ -1172,6 +1157,21 @@ int render_frames(pt_context* ctx, const pt_render_camera* cams, int frames, con
     const int units = ctx->tiling.unit_count;
     if ((long long)units * frames > kMaxFrameLaunchUnits) { set_error("too many frames for one launch"); return PT_E_ARG; }
     if (frames > 65535) { set_error("more than 65535 frames in one launch"); return PT_E_ARG; }  // the accumulate's gridDim.y
+    // every frame's accumulate runs at once (accumulate_frames_kernel, blockIdx.y = frame): the frames' buffers must
+    // not alias one another
+    {
+        std::vector<const void*> seen;
+        seen.reserve((size_t)frames * 2);
+        for (int f = 0; f < frames; f++) {
+            seen.push_back(images[f]);
+            if (images256 && images256[f]) seen.push_back(images256[f]);
+        }
+        std::sort(seen.begin(), seen.end());
+        if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) {
+            set_error("pt_render_frames: two frames share an image buffer");
+            return PT_E_ARG;
+        }
+    }
     // one upload: the frames' cameras, then the accumulate's table of image pointers {images, images256}
     const size_t cam_bytes = ((size_t)frames * sizeof(DevCamera) + 7) & ~(size_t)7;
     const size_t table_bytes = cam_bytes + (size_t)frames * 2 * sizeof(uint64_t);

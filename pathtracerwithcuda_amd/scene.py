@@ -332,8 +332,9 @@ def cornell_spheres_scene(cube_length: int = 512) -> Scene:
 
 def cornell_scene(mesh: Shape | None = None, mesh_material="diffuse_white", mesh_position=(0.0, 1.55, -1.5),
                   mesh_scale=(0.7, 0.7, 0.7), mesh_rotate=(0.0, 0.0, 0.0), spheres: bool = True,
-                  cube_length: int = 512, leaf_size: int = 1) -> Scene:
-    """res/scene/cornell_box_simple.json (walls, light, iron + glass spheres) plus an optional mesh."""
+                  cube_length: int = 512, leaf_size: int = 1, method: int = 2) -> Scene:
+    """res/scene/cornell_box_simple.json (walls, light, iron + glass spheres) plus an optional mesh. `method`: the BVH
+    builder (pt_bvh_build_method: 2 the reference's MortonCodeCUDA, 3 PT_BVH_SAH)."""
     s = Scene()
     walls = [s.add_material(m) for m in ("wall_white", "wall_green", "wall_red", "wall_white", "wall_white")]
     s.add_mesh(cornell_shapes(), walls, position=(0.0, -0.8, 1.0), scale=(0.1, 0.1, 0.3))
@@ -346,4 +347,4 @@ def cornell_scene(mesh: Shape | None = None, mesh_material="diffuse_white", mesh
         s.add_sphere((1.3, 0.0, -0.4), 0.8, "glass")
     if cube_length:
         s.set_cube_map(procedural_cube_map(cube_length))
-    return s.build(leaf_size=leaf_size)
+    return s.build(leaf_size=leaf_size, method=method)

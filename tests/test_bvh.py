@@ -223,8 +223,13 @@ def test_morton_and_clz_known_answers():
         assert L.pt_clz_table(v) == clz(v)
 
 
-def test_flattened_structure_invariants():
-    sc = pt.cornell_scene(pt.torus_knot(80, 20), cube_length=0)
+@pytest.mark.parametrize("method,leaf,order", [(2, 1, "0"), (3, 1, "0"), (3, 1, "1"), (3, 1, "2"), (3, 3, "2"),
+                                               (2, 2, "0")])
+def test_flattened_structure_invariants(monkeypatch, method, leaf, order):
+    """The reference's Morton LBVH (2) and PT_BVH_SAH (3, every child order): preorder with skip indices, every
+    triangle in exactly one leaf slot, leaves' boxes holding their triangles, children nested in their parents."""
+    monkeypatch.setenv("PT_SAH_ORDER", order)
+    sc = pt.cornell_scene(pt.torus_knot(80, 20), cube_length=0, method=method, leaf_size=leaf)
     v = sc.view
     tri_seen = np.zeros(v.triangle_num, int)
     for m in range(v.mesh_num):
@@ -237,16 +242,51 @@ def test_flattened_structure_invariants():
             assert i < d.next_node_index <= num
             if d.is_leaf:
                 assert d.next_node_index == i + 1
-                t = d.triangle_indices[0]
-                assert start <= t < start + cnt
-                tri_seen[t] += 1
-                tr = v.triangles[t]
-                for p in (tr.vertex0, tr.vertex1, tr.vertex2):
-                    assert d.box.left_bottom.x <= p.x <= d.box.right_top.x
-                    assert d.box.left_bottom.y <= p.y <= d.box.right_top.y
-                    assert d.box.left_bottom.z <= p.z <= d.box.right_top.z
+                slots = [d.triangle_indices[k] for k in range(leaf)]
+                assert slots[0] >= 0 and all(t == -1 for t in slots[slots.index(-1):]) if -1 in slots else True
+                for t in slots:
+                    if t < 0:
+                        continue
+                    assert start <= t < start + cnt
+                    tri_seen[t] += 1
+                    tr = v.triangles[t]
+                    for p in (tr.vertex0, tr.vertex1, tr.vertex2):
+                        assert d.box.left_bottom.x <= p.x <= d.box.right_top.x
+                        assert d.box.left_bottom.y <= p.y <= d.box.right_top.y
+                        assert d.box.left_bottom.z <= p.z <= d.box.right_top.z
             else:
-                # children nest inside the parent box
-                c = nodes[i + 1]
-                assert c.box.left_bottom.x >= d.box.left_bottom.x and c.box.right_top.x <= d.box.right_top.x
+                # both children nest inside the parent box: the first is the next record, the second follows the
+                # first's subtree
+                for c in (nodes[i + 1], nodes[nodes[i + 1].next_node_index]):
+                    for a in "xyz":
+                        assert getattr(c.box.left_bottom, a) >= getattr(d.box.left_bottom, a)
+                        assert getattr(c.box.right_top, a) <= getattr(d.box.right_top, a)
     assert (tri_seen == 1).all()
+
+
+def test_sah_tree_is_deterministic_and_cheaper():
+    """PT_BVH_SAH builds the same node array every time, and its surface-area cost (sum over internal nodes of
+    SA(node) / SA(root)) is below the reference Morton tree's on the bench knot."""
+    def cost(sc, m):
+        v = sc.view
+        nodes = v.bvh_nodes[m]
+
+        def sa(d):
+            x = d.box.right_top.x - d.box.left_bottom.x
+            y = d.box.right_top.y - d.box.left_bottom.y
+            z = d.box.right_top.z - d.box.left_bottom.z
+            return x * y + y * z + z * x
+        root = sa(nodes[0])
+        return sum(sa(nodes[i]) for i in range(v.mesh_node_num[m]) if not nodes[i].is_leaf) / root
+
+    def dump(sc, m):
+        v = sc.view
+        return [(d.box.left_bottom.x, d.box.right_top.z, d.next_node_index, d.is_leaf,
+                 d.triangle_indices[0] if d.is_leaf else -1)
+                for d in (v.bvh_nodes[m][i] for i in range(v.mesh_node_num[m]))]
+    knot = pt.torus_knot(60, 20)
+    a = pt.cornell_scene(knot, cube_length=0, method=3)
+    b = pt.cornell_scene(knot, cube_length=0, method=3)
+    ref = pt.cornell_scene(knot, cube_length=0, method=2)
+    assert dump(a, 2) == dump(b, 2)
+    assert cost(a, 2) < 0.95 * cost(ref, 2), (cost(a, 2), cost(ref, 2))

@@ -379,6 +379,26 @@ def test_metric_frame_at_the_bench_launch_shape(bench_gpu):
     assert launches == {0: 1, 3: 1}, launches
 
 
+@pytest.mark.parametrize("name,passes,order", [("metric", 8, "2"), ("metric", 8, "0"), ("c2", 8, "2"), ("c4", 4, "2")])
+def test_sah_tree_frames_equal_the_oracle_and_the_reference_tree(bench_gpu, monkeypatch, name, passes, order):
+    """PT_BVH_SAH (pt_host.cpp pt_bvh_build_sah: the same triangles in a true-surface-area tree, flattened as the
+    reference flattens its own): the HIP frame at the bench's launch shape equals the oracle walking the SAME tree on
+    every pixel, bit for bit, and the stated tolerance to the reference tree's frame holds: on these
+    frames the measured distance is zero, every pixel of the float running sum and of the 8-bit image equal to the
+    reference LBVH's frame (tools/tree_study.py, profiles/r06/tree/), with fewer BVH nodes per segment."""
+    import bench
+    monkeypatch.setenv("PT_SAH_ORDER", order)
+    wl = bench.Workload(name, tree="sah")
+    launches, st = _render_workload(bench_gpu, wl, passes=passes)
+    assert launches == {0: 1, 3: 1}, launches
+    ref_wl = bench.Workload(name, tree="lbvh")
+    ref, ref8, rst = oracle.render(ref_wl.scene.view, ref_wl.cam, ref_wl.cfg, 1, passes)
+    img, img8 = bench_gpu.download()
+    assert_bitwise(img.reshape(-1, 3), ref, f"{name} SAH frame vs the reference tree's, float")
+    assert_bitwise(img8.reshape(-1, 3), ref8, f"{name} SAH frame vs the reference tree's, 8-bit")
+    assert st["segments"] == rst["segments"] and st["nodes"] < rst["nodes"], (st, rst)
+
+
 def test_metric_frames_grouped_as_the_bench_times_them(bench_gpu):
     """bench.py's default timed launch at N = 1: the metric frame rendered by pt_render_frames, several frames
     per launch (pass_kernel_u's MULTI instance, one accumulate per frame), each through its own camera. Every
@@ -463,6 +483,15 @@ def test_render_frames_refuses_launches_past_its_limits(bench_gpu):
     assert 4096 * 4096 * 65 > (1 << 30)
     with pytest.raises(pt.PtError, match="too many frames"):
         r.render_frames([big] * 65, cfg, imgs, None, 1, 1, write_u8=0)
+    # every frame's running sum is accumulated at the same time: frames may not share a buffer (advisor r05)
+    r.setup_frame(8, 8)
+    small = pt.camera(8, 8, **BENCH_CAM)
+    a, b = (torch.zeros(8 * 8 * 3, dtype=torch.float32, device="cuda:0") for _ in range(2))
+    a8 = torch.zeros(8 * 8 * 3, dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(pt.PtError, match="share an image buffer"):
+        r.render_frames([small, small], cfg, [a, a], None, 1, 1, write_u8=0)
+    with pytest.raises(pt.PtError, match="share an image buffer"):
+        r.render_frames([small, small], cfg, [a, b], [a8, a8], 1, 1, write_u8=2)
     r.synchronize()
 
 

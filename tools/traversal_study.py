@@ -25,20 +25,25 @@ NAMES = ["calls", "ref_nodes", "oct_nodes", "octm_nodes", "stack_boxes", "stack_
 
 
 def main():
+    """traversal_study.py [SAMPLE [PASSES [TREE [WORKLOAD]]]]; TREE: lbvh (the reference tree) or sah<o> (PT_BVH_SAH,
+    child order o, tools/tree_study.py)."""
     sample = int(sys.argv[1]) if len(sys.argv) > 1 else 100000
     passes = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    so = "/tmp/libstudy.so"
+    tree = sys.argv[3] if len(sys.argv) > 3 else "lbvh"
+    workload = sys.argv[4] if len(sys.argv) > 4 else "metric"
+    so = f"/tmp/libstudy_{os.getpid()}.so"
     subprocess.run(["gcc", "-O2", "-std=gnu11", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fopenmp",
                     "-shared", os.path.join(ROOT, "tools", "traversal_study.c"), "-o", so, "-lm"], check=True)
     oracle.build()
     oracle.VARIANTS[""] = so
     L = oracle.lib()
     L.study_stats.argtypes = [C.c_void_p]
-    scene = pt.cornell_scene(pt.torus_knot(*bench.KNOT))
-    cfg = pt.configuration(max_tracer_depth=bench.DEPTH)
-    cam = pt.camera(bench.WIDTH, bench.HEIGHT, **bench.CAMERA)
+    if tree.startswith("sah"):
+        os.environ["PT_SAH_ORDER"] = tree[3:] or "0"
+    wl = bench.Workload(workload, tree="sah" if tree.startswith("sah") else "lbvh")
+    scene, cfg, cam = wl.scene, wl.cfg, wl.cam
     rng = np.random.default_rng(1)
-    pix = np.sort(rng.choice(bench.WIDTH * bench.HEIGHT, size=sample, replace=False)).astype(np.int32)
+    pix = np.sort(rng.choice(wl.width * wl.height, size=sample, replace=False)).astype(np.int32)
     t0 = time.time()
     oracle.render(scene.view, cam, cfg, 1, passes, pixels=pix, with_u8=False)
     st = (C.c_ulonglong * 16)()
