@@ -21,9 +21,12 @@ extern "C" int pt_device_count(void) { return 0; }
 extern "C" int pt_bvh_build_device(const pt_triangle*, int, int, int, pt_bvh_node_device**, int*, int**, int*) {
     return -1;
 }
+extern "C" int pt_bvh_build_sah_device(const pt_triangle*, int, int, int, int, pt_bvh_node_device**, int*, int**, int*) {
+    return -1;
+}
 
 static int run_scene(const char* root, const char* scene, const char* bg, const char* fmt) {
-    for (int method = 0; method < 3; method++) {
+    for (int method = 0; method < 4; method++) {  // NaiveCPU, MortonCodeCPU, MortonCodeCUDA, PT_BVH_SAH
         for (int leaf = 1; leaf <= 3; leaf += 2) {
             pt_scene_builder* b = pt_scene_builder_create();
             pt_scene_load_options o;
