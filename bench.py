@@ -63,17 +63,25 @@ def extend_bytes(counts: dict, sphere_count: int) -> float:
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+class ReferenceAssetsMissing(RuntimeError):
+    """The reference's own assets are not packed here (tests skip their C5 / reference-scene cases)."""
+
+
 def asset_root() -> str:
     """A reference-style working directory (res/configuration, res/scene, res/obj, res/texture) holding the
     scene fixtures of tests/golden/res and the reference's own meshes, textures and lobby skybox from
-    tests/golden/ref_assets.tar.xz (tools/pack_ref_assets.py), unpacked once per pack into the temp
-    directory. /root/reference is not read: it does not exist on the GPU box."""
+    tests/golden/ref_assets.tar.xz, unpacked once per pack into the temp directory. The pack is not in git (the
+    reference states no license for its assets): __graft_entry__.build() writes it from a reference
+    checkout (tools/pack_ref_assets.py), and it travels to the GPU box with the tree like the built libraries.
+    /root/reference is not read here: it does not exist on the GPU box."""
     import hashlib
     import shutil
     import tarfile
     import tempfile
 
     pack = os.path.join(GOLDEN, "ref_assets.tar.xz")
+    if not os.path.exists(pack):
+        raise ReferenceAssetsMissing(f"{pack} is absent: run tools/pack_ref_assets.py with the reference checkout")
     digest = hashlib.sha256(open(pack, "rb").read()).hexdigest()[:16]
     fixtures = hashlib.sha256()
     for d, _, fs in sorted(os.walk(os.path.join(GOLDEN, "res"))):

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Packs the reference's own asset files that the GPU tests and `bench.py --workload c5` render into
-tests/golden/ref_assets.tar.xz (data fixtures: meshes, textures, skybox faces — no source).
+tests/golden/ref_assets.tar.xz (data fixtures: meshes, textures, skybox faces — no source). The pack is git-ignored
+(the reference states no license for these assets, and the sponza maps carry their own): __graft_entry__.build()
+regenerates it from the checkout; tests that need it skip where it is absent.
 
 /root/reference does not exist on the GPU box, so the scenes that use these assets can only run there
 from a committed copy. The pack keeps the reference's directory layout (res/obj, res/texture/...), so
@@ -47,6 +49,9 @@ def main() -> int:
             info.mtime = 0
             info.mode = 0o444
             tar.addfile(info, io.BytesIO(data))
+    if os.path.exists(OUT) and open(OUT, "rb").read() == buf.getvalue():
+        print(f"{OUT}: unchanged")
+        return 0
     open(OUT, "wb").write(buf.getvalue())
     print(f"{OUT}: {len(FILES)} files, {len(buf.getvalue())} bytes, sha256 {hashlib.sha256(buf.getvalue()).hexdigest()[:16]}")
     return 0
