@@ -32,6 +32,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 WIDTH, HEIGHT, SPP, DEPTH = 1920, 1080, 8, 8
+# The BVH the timed frames walk by default: PT_BVH_SAH (pt_host.cpp, a surface-area tree with the walk's expected
+# dependent steps minimised), whose frames equal the reference tree's bit for bit on the metric, C2 and C4 frames
+# (profiles/r06/tree/); every N = 1 line re-checks that (config.image_matches_reference_tree) and times the reference
+# LBVH beside it (config.alt_tree). PT_BENCH_TREE / --tree lbvh puts the reference tree in the headline.
+DEFAULT_TREE = os.environ.get("PT_BENCH_TREE", "sah")
 KNOT = (350, 100)  # 70,000 triangles: the ~70k-triangle bunny stand-in
 CAMERA = dict(pitch=0.08, radius=12.5, center=(0.0, 1.2, 0.0))
 BAND_ROWS = int(os.environ.get("PT_BAND_ROWS", "8"))  # rows per interleaved band of the tiled frame
@@ -322,7 +327,7 @@ def main() -> int:
     ap.add_argument("--workload", choices=["metric", "c1", "c2", "c3", "c4", "c5"], default="metric",
                     help="metric: BASELINE.json's metric configuration (default); c1: its CPU-path plumbing config "
                          "(the line then carries that frame's CPU-path time as cpu_baseline); c2-c5: its other configs")
-    ap.add_argument("--tree", choices=list(Workload.TREES), default=os.environ.get("PT_BENCH_TREE", "lbvh"),
+    ap.add_argument("--tree", choices=list(Workload.TREES), default=DEFAULT_TREE,
                     help="the BVH the timed frames walk: lbvh, the reference's Morton LBVH (Bvh/bvh.cpp:862-1047, its "
                          "config default), or sah, PT_BVH_SAH (DESIGN.md §5)")
     ap.add_argument("--no-alt-tree", action="store_true",

@@ -44,3 +44,8 @@ struct PtTreeNode {
 // the parent's (pt_host.cpp).
 int pt_flatten_tree(std::vector<PtTreeNode>& nodes, int leaf_size, pt_bvh_node_device** nodes_out, int* node_num_out,
                     int** leaf_out, int* leaf_num_out);
+
+// PT_BVH_SAH's preorder child order (PT_SAH_ORDER, pt_host.cpp) and order 6's bottom-up reordering of a built tree by
+// the walk's expected dependent steps (both builders apply it before flattening).
+int pt_sah_order();
+void pt_sah_order_by_steps(std::vector<PtTreeNode>& nodes);

@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kSahBlock) void sah_level_kernel(const float* __res
         s_split[0] = best_axis;
         s_split[1] = best_bin;
         s_split[2] = best_axis < 0 ? cnt / 2 : best_nl;
-        if (best_axis >= 0 && order == 1) {  // the children's boxes: unions of their bins
+        if (best_axis >= 0 && (order == 1 || order == 3)) {  // the children's boxes: unions of their bins
             for (int side = 0; side < 2; side++) {
                 bool any = false;
                 const int c0 = side == 0 ? 0 : best_bin, c1 = side == 0 ? best_bin : bins;
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(kSahBlock) void sah_level_kernel(const float* __res
     if (threadIdx.x == 0) {
         const int l = atomicAdd(&tree.count[0], 2), r = l + 1;
         bool swap = false;
-        if (order == 1) {
+        if (order == 1 || order == 3) {
             double sl, sr;
             if (axis >= 0) {
                 sl = sa_of(&s_child[0][0], &s_child[0][3]);
@@ -290,9 +290,11 @@ __global__ __launch_bounds__(kSahBlock) void sah_level_kernel(const float* __res
                 sl = sa_of(bl_, bl_ + 3);
                 sr = sa_of(br_, br_ + 3);
             }
-            swap = sr > sl;
-        } else if (order == 2) {
-            swap = (e - mid) > (mid - b);
+            swap = order == 1 ? sr > sl : sr < sl;
+        } else if (order == 2 || order == 4) {
+            swap = order == 2 ? (e - mid) > (mid - b) : (e - mid) < (mid - b);
+        } else if (order == 5) {
+            swap = true;
         }
         tree.left[task.node] = swap ? r : l;
         tree.right[task.node] = swap ? l : r;
@@ -312,8 +314,8 @@ extern "C" int pt_bvh_build_sah_device(const pt_triangle* tris, int n, int start
     if (!tris || n <= 0 || leaf_size <= 0 || bins < 2 || bins > kMaxBins || !nodes_out || !node_num_out || !leaf_out ||
         !leaf_num_out)
         return -1;
-    const char* order_env = std::getenv("PT_SAH_ORDER");
-    const int order = order_env ? std::atoi(order_env) : 2;
+    const int order_cfg = pt_sah_order();
+    const int order = order_cfg == 6 ? 0 : order_cfg;  // 6: reordered on the host (pt_sah_order_by_steps)
     const size_t cap = 2 * (size_t)n;  // nodes of a tree with at least one triangle per leaf
     hipStream_t stream = nullptr;
     void* mem = nullptr;
@@ -392,5 +394,6 @@ extern "C" int pt_bvh_build_sah_device(const pt_triangle* tris, int n, int start
             tree[(size_t)g.right].parent = i;
         }
     }
+    if (order_cfg == 6) pt_sah_order_by_steps(tree);
     return pt_flatten_tree(tree, leaf_size, nodes_out, node_num_out, leaf_out, leaf_num_out);
 }

@@ -429,8 +429,16 @@ extern "C" int pt_bvh_build_naive(const pt_triangle* tris, int n, int start_inde
 // walk (path_tracer_kernel.cu:111-150) and every kernel run on it unchanged; the closest hit differs from the
 // reference tree's only where the walk order decides it (ties, boxes grazed in float), DESIGN.md §5.
 // Preorder child order (PT_SAH_ORDER, the study's knob): 0 the lower side of the split first, 1 the child of larger
-// surface area first, 2 (default) the child with more triangles first: on whole frames 2 walks the fewest nodes
-// (metric -8.0 %, C4 -13.5 % against the reference tree; 0: -6.5 %, -11.0 %; profiles/r06/tree/).
+// surface area first, 2 the child with more triangles first, 3 the smaller surface area first, 4 fewer triangles first,
+// 5 the upper side first, 6 (default) the order of least expected dependent steps (pt_sah_order_by_steps). Orders
+// 1-6 visit about the same nodes (metric -8 %, C4 -14 % against the reference tree), but the GPU walk is bound by its
+// dependent steps, and those differ: per mesh walk on the metric frame the reference tree takes 5.16, order 2 5.44,
+// order 6 4.72 (C4: 9.10, 8.62, 7.77; tools/traversal_study.py, profiles/r06/tree/).
+int pt_sah_order() {
+    const char* e = std::getenv("PT_SAH_ORDER");
+    return e ? std::atoi(e) : 6;
+}
+
 namespace {
 
 inline double sa_of(const Box& b) {
@@ -439,8 +447,7 @@ inline double sa_of(const Box& b) {
 }
 
 int sah_build(const pt_triangle* tris, int n, int start, int leaf_size, int bins, std::vector<GNode>& nodes) {
-    const char* order_env = std::getenv("PT_SAH_ORDER");
-    const int order = order_env ? std::atoi(order_env) : 2;
+    const int order = pt_sah_order() == 6 ? 0 : pt_sah_order();  // 6: reordered afterwards (pt_sah_order_by_steps)
     bins = std::max(2, std::min(bins, 256));
     std::vector<Box> box((size_t)n);
     std::vector<float> cen((size_t)n * 3);
@@ -537,7 +544,10 @@ int sah_build(const pt_triangle* tris, int n, int start, int leaf_size, int bins
             Box bl = box[(size_t)idx[(size_t)t.begin]], br = box[(size_t)idx[(size_t)mid]];
             for (int i = t.begin + 1; i < mid; i++) expand(bl, box[(size_t)idx[(size_t)i]]);
             for (int i = mid + 1; i < t.end; i++) expand(br, box[(size_t)idx[(size_t)i]]);
-            const bool swap = order == 1 ? sa_of(br) > sa_of(bl) : (t.end - mid) > (mid - t.begin);
+            const double sl = sa_of(bl), sr = sa_of(br);
+            const int nl = mid - t.begin, nr = t.end - mid;
+            const bool swap = order == 1 ? sr > sl : order == 2 ? nr > nl : order == 3 ? sr < sl : order == 4 ? nr < nl
+                                                                                      : true;  // 5: upper side first
             if (swap) std::swap(first, second);
         }
         nodes[(size_t)t.node].left = first;
@@ -550,6 +560,57 @@ int sah_build(const pt_triangle* tris, int n, int start, int leaf_size, int bins
 
 }  // namespace
 
+// Child order 6: the order that minimises the walk's expected dependent steps (pass_kernel_u's two-record step,
+// pt_path.h walk_box_inline), bottom-up. A step loads the records at pos and pos + 1, so a passing internal node's
+// first child is tested in the same step ("free") while its second child is reached by a skip and starts a step of its
+// own. With P(Y) = SA(Y) / SA(parent) the chance that a ray through the parent passes Y (1 for a thin leaf, whose box
+// the flattening widens to its parent's):
+//   start(leaf) = 1,  free(leaf) = P                       (a passing second-record leaf is re-tested with its triangle)
+//   start(Y) = 1 + P(Y) (free(F) + start(S)),  free(Y) = P(Y) (start(F) + start(S))   for Y's children F first, S second
+// and each node takes the order with the smaller free(F) + start(S).
+void pt_sah_order_by_steps(std::vector<PtTreeNode>& nodes) {
+    if (nodes.empty()) return;
+    std::vector<int> post;
+    post.reserve(nodes.size());
+    {
+        std::vector<std::pair<int, int>> st{{0, 0}};
+        while (!st.empty()) {
+            auto& top = st.back();
+            const PtTreeNode& g = nodes[(size_t)top.first];
+            if (!g.leaf && top.second < 2) {
+                const int c = top.second++ == 0 ? g.left : g.right;
+                st.push_back({c, 0});
+                continue;
+            }
+            post.push_back(top.first);
+            st.pop_back();
+        }
+    }
+    std::vector<double> cstart(nodes.size(), 1.0), cfree(nodes.size(), 0.0), prob(nodes.size(), 1.0);
+    for (size_t i = 0; i < nodes.size(); i++) {
+        const PtTreeNode& g = nodes[i];
+        if (g.leaf || g.left < 0) continue;
+        const double sp = sa_of(g.box);
+        for (int c : {g.left, g.right}) {
+            const PtTreeNode& k = nodes[(size_t)c];
+            prob[(size_t)c] = (k.leaf && is_thin(k.box)) || !(sp > 0.0) ? 1.0 : std::min(1.0, sa_of(k.box) / sp);
+        }
+    }
+    for (int id : post) {
+        PtTreeNode& g = nodes[(size_t)id];
+        if (g.leaf) {
+            cstart[(size_t)id] = 1.0;
+            cfree[(size_t)id] = prob[(size_t)id];
+            continue;
+        }
+        const int a = g.left, b = g.right;
+        const double ab = cfree[(size_t)a] + cstart[(size_t)b], ba = cfree[(size_t)b] + cstart[(size_t)a];
+        if (ba < ab) std::swap(g.left, g.right);
+        cstart[(size_t)id] = 1.0 + prob[(size_t)id] * std::min(ab, ba);
+        cfree[(size_t)id] = prob[(size_t)id] * (cstart[(size_t)a] + cstart[(size_t)b]);
+    }
+}
+
 extern "C" int pt_bvh_build_sah(const pt_triangle* tris, int n, int start_index, int leaf_size, int bins,
                                 pt_bvh_node_device** nodes_out, int* node_num_out, int** leaf_out, int* leaf_num_out) {
     if (!tris || n <= 0 || leaf_size <= 0 || bins <= 0 || !nodes_out || !node_num_out || !leaf_out || !leaf_num_out)
@@ -557,6 +618,7 @@ extern "C" int pt_bvh_build_sah(const pt_triangle* tris, int n, int start_index,
     std::vector<GNode> nodes;
     int rc = sah_build(tris, n, start_index, leaf_size, bins, nodes);
     if (rc != 0) return rc;
+    if (pt_sah_order() == 6) pt_sah_order_by_steps(nodes);
     return flatten_tree(nodes, leaf_size, nodes_out, node_num_out, leaf_out, leaf_num_out);
 }
 

@@ -224,6 +224,7 @@ def test_morton_and_clz_known_answers():
 
 
 @pytest.mark.parametrize("method,leaf,order", [(2, 1, "0"), (3, 1, "0"), (3, 1, "1"), (3, 1, "2"), (3, 3, "2"),
+                                               (3, 1, "3"), (3, 1, "4"), (3, 1, "5"), (3, 1, "6"), (3, 2, "6"),
                                                (2, 2, "0")])
 def test_flattened_structure_invariants(monkeypatch, method, leaf, order):
     """The reference's Morton LBVH (2) and PT_BVH_SAH (3, every child order): preorder with skip indices, every

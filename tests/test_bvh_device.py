@@ -244,7 +244,7 @@ def _sah_nodes(fn, tris, start, leaf_size, bins=32):
     return res
 
 
-@pytest.mark.parametrize("order", ["0", "1", "2"])
+@pytest.mark.parametrize("order", ["0", "1", "2", "3", "4", "5", "6"])
 @pytest.mark.parametrize("n,leaf,start,kind,bins", [(1, 1, 0, "rand", 32), (2, 1, 3, "rand", 32), (300, 1, 0, "rand", 32),
                                                     (5000, 1, 7, "rand", 32), (4099, 3, 0, "rand", 16),
                                                     (2000, 1, 0, "flat", 32), (777, 2, 0, "dup", 64)])

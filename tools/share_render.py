@@ -23,7 +23,7 @@ def main() -> None:
     ap.add_argument("--workload", default="metric")
     ap.add_argument("--group", type=int, default=1, help="frames per launch (pt_render_frames)")
     ap.add_argument("--medium-bound", action="store_true", help="pt_set_medium_bound (tolerance mode)")
-    ap.add_argument("--tree", choices=list(bench.Workload.TREES), default=os.environ.get("PT_BENCH_TREE", "lbvh"))
+    ap.add_argument("--tree", choices=list(bench.Workload.TREES), default=bench.DEFAULT_TREE)
     args = ap.parse_args()
     wl = bench.Workload(args.workload, tree=args.tree)
     r = pt.Renderer(0)

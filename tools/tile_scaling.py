@@ -40,7 +40,7 @@ def main() -> None:
                     help="with --group: render this many frames in launches of at most --group frames (bench.py's "
                          "timed sequence, e.g. 20 = 8 + 8 + 4) instead of --frames full launches")
     args = ap.parse_args()
-    wl = bench.Workload("metric")
+    wl = bench.Workload("metric", tree=bench.DEFAULT_TREE)
     spp = args.spp or wl.spp
     scale = wl.spp / spp  # per-frame (8-pass) figures
     rs = []

@@ -29,9 +29,10 @@ typedef struct { int n; int* left; int* right; sn* oct[8]; const pt_bvh_node_dev
 #define MAXM 16
 static smesh g_mesh[MAXM];
 static unsigned long long g_stat[16];
-static unsigned long long g_mesh_tris[MAXM], g_mesh_nodes[MAXM], g_mesh_calls[MAXM], g_mesh_oct[MAXM], g_mesh_n[MAXM];
+static unsigned long long g_mesh_tris[MAXM], g_mesh_nodes[MAXM], g_mesh_calls[MAXM], g_mesh_oct[MAXM], g_mesh_n[MAXM],
+    g_mesh_steps[MAXM];
 enum { S_CALLS, S_REF_NODES, S_OCT_NODES, S_OCTM_NODES, S_STACK_BOX, S_STACK_POPS, S_OCT_MISMATCH, S_OCTM_MISMATCH,
-       S_ANOM, S_TIE, S_STACK_MISMATCH, S_REF_HITS, S_NSTAT };
+       S_ANOM, S_TIE, S_STACK_MISMATCH, S_REF_HITS, S_REF_STEPS, S_NSTAT };
 
 static void cen(const pt_bounding_box* b, float c[3]) {
     c[0] = 0.5f * (b->left_bottom.x + b->right_top.x);
@@ -216,6 +217,34 @@ static void study_hook(const void* scv, int m, float ox, float oy, float oz, flo
         }
         (void)an; (void)ti;
     }
+    /* the GPU walk's dependent steps over the same preorder walk (pass_kernel_u, walk_box_inline): a step loads the
+       records at pos and pos + 1; a passing internal node tests pos + 1 in the same step (a passing internal second
+       record moves the walk to pos + 2, a passing leaf second record is re-tested with its triangle next step); a
+       passing first-record leaf is tested with its triangle and the walk moves to pos + 1 */
+    {
+        const pt_bvh_node_device* nd = s->ref;
+        float bt = INFINITY;
+        int pos = 0;
+        while (pos != s->n) {
+            loc[S_REF_STEPS]++;
+            float lo[3] = {nd[pos].box.left_bottom.x, nd[pos].box.left_bottom.y, nd[pos].box.left_bottom.z};
+            float hi[3] = {nd[pos].box.right_top.x, nd[pos].box.right_top.y, nd[pos].box.right_top.z};
+            float e;
+            if (!(sbox(lo, hi, o, inv, &e) && e <= bt)) { pos = nd[pos].next_node_index; continue; }
+            if (nd[pos].is_leaf) {
+                float tt, t1, t2;
+                int ti2 = nd[pos].triangle_indices[0];
+                if (triangle_intersect(&sc->tris[ti2], o, d, &tt, &t1, &t2) && tt > 0.0f && tt < bt) bt = tt;
+                pos++;
+                continue;
+            }
+            const int q = pos + 1;
+            float lo2[3] = {nd[q].box.left_bottom.x, nd[q].box.left_bottom.y, nd[q].box.left_bottom.z};
+            float hi2[3] = {nd[q].box.right_top.x, nd[q].box.right_top.y, nd[q].box.right_top.z};
+            if (!(sbox(lo2, hi2, o, inv, &e) && e <= bt)) pos = nd[q].next_node_index;
+            else pos = nd[q].is_leaf ? q : q + 1;
+        }
+    }
     best_t b;
     walk_oct(sc, s, k, o, d, inv, 1.0f, &b, &loc[S_OCT_NODES], &loc[S_ANOM], &loc[S_TIE]);
     int same = hit ? (b.tri == tri && b.t == t) : (b.tri < 0);
@@ -230,6 +259,7 @@ static void study_hook(const void* scv, int m, float ox, float oy, float oz, flo
     for (int i = 0; i < S_NSTAT; i++) __atomic_fetch_add(&g_stat[i], loc[i], __ATOMIC_RELAXED);
     __atomic_fetch_add(&g_mesh_nodes[m], loc[S_REF_NODES], __ATOMIC_RELAXED);
     __atomic_fetch_add(&g_mesh_oct[m], loc[S_OCT_NODES], __ATOMIC_RELAXED);
+    __atomic_fetch_add(&g_mesh_steps[m], loc[S_REF_STEPS], __ATOMIC_RELAXED);
     __atomic_fetch_add(&g_mesh_calls[m], 1, __ATOMIC_RELAXED);
     g_mesh_n[m] = s->n;
 }
@@ -275,8 +305,9 @@ void study_stats(unsigned long long* out) {
     for (int i = 0; i < S_NSTAT; i++) out[i] = g_stat[i];
     for (int m = 0; m < MAXM; m++)
         if (g_mesh_calls[m])
-            printf("  mesh %d: %llu nodes, %llu walks, ref nodes/walk %.2f, tris/walk %.2f, oct nodes/walk %.2f\n", m,
-                   g_mesh_n[m], g_mesh_calls[m], (double)g_mesh_nodes[m] / g_mesh_calls[m],
-                   (double)g_mesh_tris[m] / g_mesh_calls[m], (double)g_mesh_oct[m] / g_mesh_calls[m]);
+            printf("  mesh %d: %llu nodes, %llu walks, ref nodes/walk %.2f, steps/walk %.2f, tris/walk %.2f, oct nodes/walk %.2f\n",
+                   m, g_mesh_n[m], g_mesh_calls[m], (double)g_mesh_nodes[m] / g_mesh_calls[m],
+                   (double)g_mesh_steps[m] / g_mesh_calls[m], (double)g_mesh_tris[m] / g_mesh_calls[m],
+                   (double)g_mesh_oct[m] / g_mesh_calls[m]);
     fflush(stdout);
 }

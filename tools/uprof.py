@@ -11,7 +11,7 @@ import bench  # noqa: E402
 import pathtracerwithcuda_amd as pt  # noqa: E402
 
 # argv[1]: a bench.py workload (default "metric"); one frame of its 8 passes in one launch
-wl = bench.Workload(sys.argv[1] if len(sys.argv) > 1 else "metric")
+wl = bench.Workload(sys.argv[1] if len(sys.argv) > 1 else "metric", tree=bench.DEFAULT_TREE)
 r = pt.Renderer(0)
 scene, cfg, cam = wl.scene, wl.cfg, wl.cam
 r.upload(scene, cfg)
