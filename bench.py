@@ -674,7 +674,7 @@ def main() -> int:
     workload = wl.key
     # profiles/traffic.json keys: the workload, then "/sah" for the PT_BVH_SAH tree (the reference tree unsuffixed)
     suffix = ("" if schedule == "persistent" else "/wavefront") + ("/medium_bound" if args.medium_bound else "")
-    key = workload + ("/sah" if args.tree == "sah" else "") + suffix
+    key = workload + ("/sah" if args.tree == "sah" and scene.view.mesh_num > 0 else "") + suffix
     # N > 1: rank 0's share profiled on its own (tools/gpu_share_pmc.sh, "<key>/tiled<N>"); otherwise the
     # whole 1-GPU frame's profile, of which a rank of N runs 1/N
     prof = load_profile(f"{key}/tiled{world}") if world > 1 else {}
@@ -786,7 +786,7 @@ def main() -> int:
         rf.update(bound="hbm", achieved=hbm["achieved"], peak=hbm["peak"], unit=hbm["unit"], frac=hbm["frac"])
     line["config"]["tree"] = args.tree
     if alt is not None:
-        aprof = load_profile(alt["key"] + ("/sah" if alt["tree"] == "sah" else "") + suffix)
+        aprof = load_profile(alt["key"] + ("/sah" if alt["tree"] == "sah" and scene.view.mesh_num > 0 else "") + suffix)
         a_valu = aprof.get("valu_insts_per_launch")
         a_hbm = aprof.get("hbm_bytes_per_launch")
         a_vf = float(a_valu) / alt["avg_launch_s"] / 1e9 / valu_peak if a_valu else None
