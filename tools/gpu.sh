@@ -70,11 +70,11 @@ workloads)
   timeout -k 10 600 python3 bench.py --workload c4 --medium-bound --no-cpu-baseline > $T/wl_c4_mb.json 2> $T/wl_c4_mb.err || exit $?
   line $T/wl_c4_mb.json c4_medium_bound ;;
 profile)
-  B="python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline"
+  B="python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-alt-tree"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $T/trace_timed -o run -- $B > $T/trace_timed.log 2>&1 || exit $?
   export PT_BENCH_INFLIGHT=1 PT_BENCH_GROUP=1  # one frame per launch, one at a time: the roofline's solo launch
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $T/trace -o run -- python3 bench.py --steps 10 --warmup 1 --no-cpu-baseline > $T/trace.log 2>&1 || exit $?
-  P="python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $T/trace -o run -- python3 bench.py --steps 10 --warmup 1 --no-cpu-baseline --no-alt-tree > $T/trace.log 2>&1 || exit $?
+  P="python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline --no-alt-tree"
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $T/pmc_fetch -o run -- $P > $T/pmc_fetch.log 2>&1 || exit $?
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $T/pmc_write -o run -- $P > $T/pmc_write.log 2>&1 || exit $?
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $T/pmc_sq -o run -- $P > $T/pmc_sq.log 2>&1 || exit $?
@@ -90,7 +90,7 @@ wlprofile)
   #   python tools/traffic_summary.py gpurun_out/<tag>/<w> profiles/<round>/workloads/<w> --workload <key> --kernel "pass_kernel_u<"
   export PT_BENCH_INFLIGHT=1 PT_BENCH_GROUP=1
   for w in ${WORKLOADS:-c1 c2 c3 c4 c4mb c5}; do
-    a="--workload ${w%mb} --no-cpu-baseline"; [ "$w" = c4mb ] && a="$a --medium-bound"
+    a="--workload ${w%mb} --no-cpu-baseline --no-alt-tree"; [ "$w" = c4mb ] && a="$a --medium-bound"
     st="--steps 3 --warmup 1"; sp="--steps 1 --warmup 0"
     case $w in c1) st="--steps 40 --warmup 2"; sp="--steps 4 --warmup 0" ;; c5) st="--steps 1 --warmup 0" ;; esac
     mkdir -p $T/$w
