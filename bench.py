@@ -292,6 +292,8 @@ def rank_breakdown(dist, frames, world: int, device) -> dict:
     n = len(t)
     mine = [sum(a for a, _ in t) / max(n, 1), sum(b for _, b in t) / max(n, 1),
             max((a for a, _ in t), default=0.0), max((b for _, b in t), default=0.0), float(n)]
+    if dist.get_backend() == "gloo":  # the rehearsal's gloo group: host tensors
+        device = "cpu"
     x = torch.tensor(mine, dtype=torch.float64, device=device)
     parts = [torch.zeros_like(x) for _ in range(world)]
     dist.all_gather(parts, x)
