@@ -574,6 +574,12 @@ def main() -> int:
     # single-frame latency (one frame at a time, host-synchronised), reported beside the throughput; the
     # dominant kernel's launch duration for the roofline is taken here too, with no other frame in flight
     # (with frames in flight the HIP events of one launch also span the overlapping launch's work)
+    # --save-image: the last timed launch's first frame (the frame the self-check compares), taken before the latency
+    # frames and the other tree's leg reuse the contexts
+    saved8 = None
+    if args.save_image and rank == 0:
+        ctx_s, _ = last_launch
+        _, saved8 = frames[ctx_s].download(0) if group > 1 else frames[ctx_s].download()
     watch.stage("single-frame latency")
     lat_frames = max(3, min(5, args.steps))
     r.set_grid_share(100)
@@ -650,11 +656,9 @@ def main() -> int:
         return 0
     watch.stage("report")
 
-    if args.save_image:  # the last timed launch's first frame (the frame the self-check compares)
+    if saved8 is not None:
         from pathtracerwithcuda_amd.imageio import write_png
-        ctx, _ = last_launch
-        _, img8 = frames[ctx].download(0) if group > 1 else frames[ctx].download()
-        write_png(args.save_image, np.asarray(img8).reshape(height, width, 3))
+        write_png(args.save_image, np.asarray(saved8).reshape(height, width, 3))
 
     value = segments / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1000.0

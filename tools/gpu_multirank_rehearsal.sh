@@ -13,7 +13,7 @@ timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --save-
 run() {  # name ranks port extra-env...
   m=$1; n=$2; port=$3; shift 3
   env "$@" PT_BENCH_BACKEND=gloo PT_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $port bench.py --gpus $n --steps ${S:-5} --warmup 1 --save-image gpurun_out/$TAG/$m.png > gpurun_out/$TAG/$m.json 2> gpurun_out/$TAG/$m.err || exit $?
-  python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], 'ranks: image_matches_1gpu', d['config']['image_matches_1gpu'], 'frames per launch', d['config']['frames_per_launch'], d['value'], 'Mrays/s')" gpurun_out/$TAG/$m.json $n
+  python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); c=d['config']; pr=c.get('per_rank') or {}; print(sys.argv[2], 'ranks: image_matches_1gpu', c['image_matches_1gpu'], 'frames per launch', c['frames_per_launch'], c['collective']['frame_collective'], d['value'], 'Mrays/s', 'render/collective ms per launch (max over ranks)', pr.get('render_ms_per_launch_max_over_ranks'), pr.get('collective_ms_per_launch_max_over_ranks'))" gpurun_out/$TAG/$m.json $n
   cmp gpurun_out/$TAG/n1.png gpurun_out/$TAG/$m.png || exit 4
 }
 # b*: one frame per launch (PT_BENCH_GROUP=1); g*: the default frame groups at N > 1 (8 N frames per launch,
