@@ -48,4 +48,5 @@ int pt_flatten_tree(std::vector<PtTreeNode>& nodes, int leaf_size, pt_bvh_node_d
 // PT_BVH_SAH's preorder child order (PT_SAH_ORDER, pt_host.cpp) and order 6's bottom-up reordering of a built tree by
 // the walk's expected dependent steps (both builders apply it before flattening).
 int pt_sah_order();
+int pt_sah_bins();
 void pt_sah_order_by_steps(std::vector<PtTreeNode>& nodes);

@@ -434,6 +434,12 @@ extern "C" int pt_bvh_build_naive(const pt_triangle* tris, int n, int start_inde
 // 1-6 visit about the same nodes (metric -8 %, C4 -14 % against the reference tree), but the GPU walk is bound by its
 // dependent steps, and those differ: per mesh walk on the metric frame the reference tree takes 5.16, order 2 5.44,
 // order 6 4.72 (C4: 9.10, 8.62, 7.77; tools/traversal_study.py, profiles/r06/tree/).
+int pt_sah_bins() {  // centroid bins per axis (PT_SAH_BINS, the study's knob; 2..64)
+    const char* e = std::getenv("PT_SAH_BINS");
+    const int b = e ? std::atoi(e) : 32;
+    return b < 2 ? 2 : (b > 64 ? 64 : b);
+}
+
 int pt_sah_order() {
     const char* e = std::getenv("PT_SAH_ORDER");
     return e ? std::atoi(e) : 6;
@@ -627,7 +633,8 @@ extern "C" int pt_bvh_build_ex(const pt_triangle* tris, int n, int start_index, 
     if (method == PT_BVH_NAIVE_CPU)
         return pt_bvh_build_naive(tris, n, start_index, leaf_size, bucket_num, nodes_out, node_num_out, leaf_out, leaf_num_out);
     if (method == PT_BVH_SAH)
-        return pt_bvh_build_sah(tris, n, start_index, leaf_size, 32, nodes_out, node_num_out, leaf_out, leaf_num_out);
+        return pt_bvh_build_sah(tris, n, start_index, leaf_size, pt_sah_bins(), nodes_out, node_num_out, leaf_out,
+                                leaf_num_out);
     // MortonCodeCPU and MortonCodeCUDA build the same tree (Bvh/bvh.cpp:667-780 vs :862-1047); the
     // CPU variant's std::sort is not stable, so equal codes keep their input order here as in the
     // CUDA variant's merge sort.
@@ -826,7 +833,8 @@ int build_mesh_bvh(pt_scene_builder* b, size_t m, pt_bvh_node_device** nodes, in
     if (device && b->build_method == PT_BVH_MORTON_CODE_CUDA)
         return pt_bvh_build_device(t, b->mesh_count[m], b->mesh_start[m], b->build_leaf, nodes, nn, leaf, ln);
     if (device && b->build_method == PT_BVH_SAH && b->mesh_count[m] >= 4096)
-        return pt_bvh_build_sah_device(t, b->mesh_count[m], b->mesh_start[m], b->build_leaf, 32, nodes, nn, leaf, ln);
+        return pt_bvh_build_sah_device(t, b->mesh_count[m], b->mesh_start[m], b->build_leaf, pt_sah_bins(), nodes, nn,
+                                       leaf, ln);
     return pt_bvh_build_ex(t, b->mesh_count[m], b->mesh_start[m], b->build_leaf, b->build_method, b->build_bucket,
                            nodes, nn, leaf, ln);
 }

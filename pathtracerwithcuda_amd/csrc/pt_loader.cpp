@@ -695,8 +695,10 @@ extern "C" int pt_config_load(const char* path, pt_configuration* cfg) {
     {  // parse_bvh_build_method (Bvh/bvh_build_config.cpp:7-27): case-insensitive, default NaiveCPU
         std::string m = v["BvhBuildMethod"];
         std::transform(m.begin(), m.end(), m.begin(), [](unsigned char ch) { return (char)std::tolower(ch); });
+        // "SAH" (not a reference value): PT_BVH_SAH, this build's surface-area tree; every other
+        // unknown value falls back to NaiveCPU as in the reference
         c.bvh_build = m == "mortoncodecpu" ? PT_BVH_MORTON_CODE_CPU
-                    : m == "mortoncodecuda" ? PT_BVH_MORTON_CODE_CUDA : PT_BVH_NAIVE_CPU;
+                    : m == "mortoncodecuda" ? PT_BVH_MORTON_CODE_CUDA : m == "sah" ? PT_BVH_SAH : PT_BVH_NAIVE_CPU;
     }
     c.air_refraction_index = parse_float(v["AirRefractionIndex"]);
     c.air_absorption_coef = parse_float3(v["AirAbsorptionCoef"]);

@@ -131,6 +131,8 @@ def test_config_quirks_and_errors(tmp_path):
     assert (c.air_absorption_coef.x, c.air_absorption_coef.y, c.air_absorption_coef.z) == (0.5, 0.25, 0.0)
     p.write_text(json.dumps(dict(src, BvhBuildMethod="whatever")))
     assert pt.load_config(str(p)).bvh_build == 0  # unknown -> NaiveCPU (bvh_build_config.cpp:26)
+    p.write_text(json.dumps(dict(src, BvhBuildMethod="Sah")))
+    assert pt.load_config(str(p)).bvh_build == 3  # this build's PT_BVH_SAH (not a reference value)
     bad = dict(src)
     del bad["SSSThreshold"]
     p.write_text(json.dumps(bad))
