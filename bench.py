@@ -598,7 +598,7 @@ def main() -> int:
     # the same way (warm-up, K timed frames, one-frame-in-flight launches for the roofline), and one frame of each
     # compared bit for bit (the trees' closest hits differ only where the walk order decides them)
     alt = None
-    if world == 1 and not distributed and not args.no_alt_tree:
+    if world == 1 and not distributed and not args.no_alt_tree and scene.view.mesh_num > 0:  # (no BVH, no tree)
         alt_tree = "lbvh" if args.tree == "sah" else "sah"
         awl = Workload(args.workload, tree=alt_tree)
         for q in rs:
