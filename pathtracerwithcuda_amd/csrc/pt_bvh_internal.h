@@ -50,3 +50,5 @@ int pt_flatten_tree(std::vector<PtTreeNode>& nodes, int leaf_size, pt_bvh_node_d
 int pt_sah_order();
 int pt_sah_bins();
 void pt_sah_order_by_steps(std::vector<PtTreeNode>& nodes);
+// the tree study's treelet restructuring (pt_host.cpp; PT_SAH_TREELET / PT_LBVH_TREELET)
+void pt_treelet_restructure(std::vector<PtTreeNode>& nodes, int k);

@@ -617,6 +617,99 @@ void pt_sah_order_by_steps(std::vector<PtTreeNode>& nodes) {
     }
 }
 
+// Treelet restructuring (Karras & Aila 2013, "Fast parallel construction of high-quality BVHs"), the study's knob
+// PT_SAH_TREELET = k (treelet leaves, 3..8; 0 off): every internal node, children first, becomes the root of a
+// treelet grown by opening its largest-area treelet leaf until k leaves; the treelet's topology is rebuilt as the one
+// of least total internal surface area (dynamic programming over the 2^k leaf subsets), reusing its internal nodes.
+void pt_treelet_restructure(std::vector<PtTreeNode>& nodes, int k) {
+    if (k < 3 || nodes.size() < 3) return;
+    k = std::min(k, 8);
+    std::vector<int> post;
+    {
+        std::vector<std::pair<int, int>> st{{0, 0}};
+        while (!st.empty()) {
+            auto& top = st.back();
+            const PtTreeNode& g = nodes[(size_t)top.first];
+            if (!g.leaf && top.second < 2) {
+                const int c = top.second++ == 0 ? g.left : g.right;
+                st.push_back({c, 0});
+                continue;
+            }
+            post.push_back(top.first);
+            st.pop_back();
+        }
+    }
+    const int full = 1 << k;
+    std::vector<Box> ubox((size_t)full);
+    std::vector<double> best((size_t)full);
+    std::vector<int> split((size_t)full);
+    for (int root : post) {
+        if (nodes[(size_t)root].leaf) continue;
+        std::vector<int> L{nodes[(size_t)root].left, nodes[(size_t)root].right}, I{root};
+        while ((int)L.size() < k) {
+            int pick = -1;
+            double area = -1.0;
+            for (int i = 0; i < (int)L.size(); i++) {
+                const PtTreeNode& g = nodes[(size_t)L[(size_t)i]];
+                if (g.leaf) continue;
+                const double a = sa_of(g.box);
+                if (a > area) { area = a; pick = i; }
+            }
+            if (pick < 0) break;
+            const int id = L[(size_t)pick];
+            L.erase(L.begin() + pick);
+            L.push_back(nodes[(size_t)id].left);
+            L.push_back(nodes[(size_t)id].right);
+            I.push_back(id);
+        }
+        const int n = (int)L.size();
+        if (n < 3) continue;
+        const int all = (1 << n) - 1;
+        for (int S = 1; S <= all; S++) {
+            const int low = __builtin_ctz((unsigned)S);
+            const int rest = S & (S - 1);
+            ubox[(size_t)S] = nodes[(size_t)L[(size_t)low]].box;
+            if (rest) expand(ubox[(size_t)S], ubox[(size_t)rest]);
+            if (!rest) { best[(size_t)S] = 0.0; continue; }
+            // the partitions {P, S \ P} with P holding S's lowest leaf
+            double b = INFINITY;
+            int bp = 0;
+            const int lowbit = S & -S;
+            for (int P = (S - 1) & S; P; P = (P - 1) & S) {
+                if (!(P & lowbit)) continue;
+                const double c = best[(size_t)P] + best[(size_t)(S ^ P)];
+                if (c < b) { b = c; bp = P; }
+            }
+            best[(size_t)S] = b + sa_of(ubox[(size_t)S]);
+            split[(size_t)S] = bp;
+        }
+        // rebuild: subset `all` at `root`, the internal nodes of the other subsets in the freed slots
+        size_t next_slot = 1;
+        std::vector<std::pair<int, int>> work{{all, root}};
+        while (!work.empty()) {
+            const auto [S, id] = work.back();
+            work.pop_back();
+            PtTreeNode& g = nodes[(size_t)id];
+            g.box = ubox[(size_t)S];
+            g.leaf = false;
+            const int P = split[(size_t)S], Q = S ^ P;
+            int child[2];
+            int sub[2] = {P, Q};
+            for (int side = 0; side < 2; side++) {
+                if ((sub[side] & (sub[side] - 1)) == 0) {
+                    child[side] = L[(size_t)__builtin_ctz((unsigned)sub[side])];
+                } else {
+                    child[side] = I[next_slot++];
+                    work.push_back({sub[side], child[side]});
+                }
+                nodes[(size_t)child[side]].parent = id;
+            }
+            g.left = child[0];
+            g.right = child[1];
+        }
+    }
+}
+
 extern "C" int pt_bvh_build_sah(const pt_triangle* tris, int n, int start_index, int leaf_size, int bins,
                                 pt_bvh_node_device** nodes_out, int* node_num_out, int** leaf_out, int* leaf_num_out) {
     if (!tris || n <= 0 || leaf_size <= 0 || bins <= 0 || !nodes_out || !node_num_out || !leaf_out || !leaf_num_out)
@@ -624,6 +717,7 @@ extern "C" int pt_bvh_build_sah(const pt_triangle* tris, int n, int start_index,
     std::vector<GNode> nodes;
     int rc = sah_build(tris, n, start_index, leaf_size, bins, nodes);
     if (rc != 0) return rc;
+    if (const char* e = std::getenv("PT_SAH_TREELET")) pt_treelet_restructure(nodes, std::atoi(e));
     if (pt_sah_order() == 6) pt_sah_order_by_steps(nodes);
     return flatten_tree(nodes, leaf_size, nodes_out, node_num_out, leaf_out, leaf_num_out);
 }
@@ -638,7 +732,30 @@ extern "C" int pt_bvh_build_ex(const pt_triangle* tris, int n, int start_index, 
     // MortonCodeCPU and MortonCodeCUDA build the same tree (Bvh/bvh.cpp:667-780 vs :862-1047); the
     // CPU variant's std::sort is not stable, so equal codes keep their input order here as in the
     // CUDA variant's merge sort.
-    return pt_bvh_build(tris, n, start_index, leaf_size, method, nodes_out, node_num_out, leaf_out, leaf_num_out);
+    const int rc = pt_bvh_build(tris, n, start_index, leaf_size, method, nodes_out, node_num_out, leaf_out, leaf_num_out);
+    // the tree study's "LBVH + treelet restructuring" (PT_LBVH_TREELET = k, off by default; never the reference
+    // tree): the flattened Morton tree read back into a linked tree, restructured, flattened again
+    const char* tl = std::getenv("PT_LBVH_TREELET");
+    if (rc != 0 || !tl || std::atoi(tl) < 3) return rc;
+    const pt_bvh_node_device* fl = *nodes_out;
+    const int nn = *node_num_out;
+    std::vector<GNode> g((size_t)nn);
+    for (int i = 0; i < nn; i++) {
+        g[(size_t)i].box = Box{{fl[i].box.left_bottom.x, fl[i].box.left_bottom.y, fl[i].box.left_bottom.z},
+                               {fl[i].box.right_top.x, fl[i].box.right_top.y, fl[i].box.right_top.z}};
+        g[(size_t)i].leaf = fl[i].is_leaf != 0;
+        if (g[(size_t)i].leaf) {
+            g[(size_t)i].tris.assign(fl[i].triangle_indices, fl[i].triangle_indices + leaf_size);
+        } else {
+            g[(size_t)i].left = i + 1;
+            g[(size_t)i].right = fl[i + 1].next_node_index;
+            g[(size_t)(i + 1)].parent = g[(size_t)fl[i + 1].next_node_index].parent = i;
+        }
+    }
+    pt_bvh_free(*nodes_out, *leaf_out);
+    pt_treelet_restructure(g, std::atoi(tl));
+    if (pt_sah_order() == 6) pt_sah_order_by_steps(g);
+    return flatten_tree(g, leaf_size, nodes_out, node_num_out, leaf_out, leaf_num_out);
 }
 
 // ---- scene assembly ----------------------------------------------------------------------------

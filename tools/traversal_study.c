@@ -32,7 +32,7 @@ static unsigned long long g_stat[16];
 static unsigned long long g_mesh_tris[MAXM], g_mesh_nodes[MAXM], g_mesh_calls[MAXM], g_mesh_oct[MAXM], g_mesh_n[MAXM],
     g_mesh_steps[MAXM];
 enum { S_CALLS, S_REF_NODES, S_OCT_NODES, S_OCTM_NODES, S_STACK_BOX, S_STACK_POPS, S_OCT_MISMATCH, S_OCTM_MISMATCH,
-       S_ANOM, S_TIE, S_STACK_MISMATCH, S_REF_HITS, S_REF_STEPS, S_NSTAT };
+       S_ANOM, S_TIE, S_STACK_MISMATCH, S_REF_HITS, S_REF_STEPS, S_CHAIN_STEPS, S_CHAIN_LEN, S_NSTAT };
 
 static void cen(const pt_bounding_box* b, float c[3]) {
     c[0] = 0.5f * (b->left_bottom.x + b->right_top.x);
@@ -227,6 +227,43 @@ static void study_hook(const void* scv, int m, float ox, float oy, float oz, flo
         int pos = 0;
         while (pos != s->n) {
             loc[S_REF_STEPS]++;
+            float lo[3] = {nd[pos].box.left_bottom.x, nd[pos].box.left_bottom.y, nd[pos].box.left_bottom.z};
+            float hi[3] = {nd[pos].box.right_top.x, nd[pos].box.right_top.y, nd[pos].box.right_top.z};
+            float e;
+            if (!(sbox(lo, hi, o, inv, &e) && e <= bt)) { pos = nd[pos].next_node_index; continue; }
+            if (nd[pos].is_leaf) {
+                float tt, t1, t2;
+                int ti2 = nd[pos].triangle_indices[0];
+                if (triangle_intersect(&sc->tris[ti2], o, d, &tt, &t1, &t2) && tt > 0.0f && tt < bt) bt = tt;
+                pos++;
+                continue;
+            }
+            const int q = pos + 1;
+            float lo2[3] = {nd[q].box.left_bottom.x, nd[q].box.left_bottom.y, nd[q].box.left_bottom.z};
+            float hi2[3] = {nd[q].box.right_top.x, nd[q].box.right_top.y, nd[q].box.right_top.z};
+            if (!(sbox(lo2, hi2, o, inv, &e) && e <= bt)) pos = nd[q].next_node_index;
+            else pos = nd[q].is_leaf ? q : q + 1;
+        }
+    }
+    /* the same steps when the walk first skips the preorder chain root, root + 1, ... of internal nodes whose boxes
+       hold the ray origin strictly inside (every such box passes: entry <= 0 < exit, and min_t is +inf at a mesh
+       walk's start), at most CHAIN nodes; the root's own test is the segment start's (not counted as a step) */
+    {
+        const int CHAIN = 4;
+        const pt_bvh_node_device* nd = s->ref;
+        int pos = 0, len = 0;
+        while (len < CHAIN && pos < s->n && !nd[pos].is_leaf) {
+            const pt_bounding_box* bb = &nd[pos].box;
+            if (!(bb->left_bottom.x < ox && ox < bb->right_top.x && bb->left_bottom.y < oy && oy < bb->right_top.y &&
+                  bb->left_bottom.z < oz && oz < bb->right_top.z))
+                break;
+            pos++;
+            len++;
+        }
+        loc[S_CHAIN_LEN] += len;
+        float bt = INFINITY;
+        while (pos != s->n) {
+            loc[S_CHAIN_STEPS]++;
             float lo[3] = {nd[pos].box.left_bottom.x, nd[pos].box.left_bottom.y, nd[pos].box.left_bottom.z};
             float hi[3] = {nd[pos].box.right_top.x, nd[pos].box.right_top.y, nd[pos].box.right_top.z};
             float e;

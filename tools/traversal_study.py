@@ -21,7 +21,7 @@ import oracle  # noqa: E402
 import pathtracerwithcuda_amd as pt  # noqa: E402
 
 NAMES = ["calls", "ref_nodes", "oct_nodes", "octm_nodes", "stack_boxes", "stack_pops", "oct_mismatch",
-         "octm_mismatch", "anomalies", "ties", "stack_mismatch", "ref_hits", "ref_steps"]
+         "octm_mismatch", "anomalies", "ties", "stack_mismatch", "ref_hits", "ref_steps", "chain_steps", "chain_len"]
 
 
 def main():
