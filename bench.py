@@ -10,7 +10,8 @@ gather per group (torch.distributed "nccl"; the float running sums stay on their
 float image stays on the device; --collective gather moves them too, --collective reduce sums the float stack on
 rank 0, the north star's RCCL reduce). Each rank of a multi-GPU run works under a stage watchdog and a collective
 timeout (--stage-timeout, 180 s): a rank stuck in a stage exits 124 with a stderr line naming it and the stage, and
-the line reports every rank's render and collective time per launch (config.per_rank).
+the line reports every rank's render and collective time per launch (config.per_rank). With the default gather8 the
+same frames are then timed again with the reduce (config.collective.reduce_leg; PT_BENCH_REDUCE_LEG=0 skips it).
 The host-synchronised single-frame latency is reported beside it. Mrays/s = ray segments traced (the live-ray counts the
 reference's thread_shrink returns, summed over passes and depths and over ranks) / wall time.
 
@@ -594,6 +595,45 @@ def main() -> int:
     latency = (time.perf_counter() - t1) / max(lat_frames, 1)
     solo_ms, solo_launches = r.kernel_time_kind(kind)
 
+    # The north star's collective beside the default (N > 1 with frame groups): the same K frames with
+    # "reduce" (every rank's float stack summed on rank 0, which then writes the 8-bit images) in place of "gather8",
+    # timed the same way (warm-up, barrier, max over ranks) on the same contexts; config.collective.reduce_leg
+    reduce_leg = None
+    if distributed and world > 1 and group > 1 and collective == "gather8" \
+            and os.environ.get("PT_BENCH_REDUCE_LEG", "1") != "0":
+        watch.stage("reduce leg")
+        for f in frames:
+            f.collective = "reduce"
+        try:
+            run(max(1, args.warmup))
+            torch.cuda.synchronize()
+            for q in rs:
+                q.stats_reset()
+            for f in frames:
+                f.clock.reset()
+            dist.barrier()
+            torch.cuda.synchronize()
+            tr = time.perf_counter()
+            run(args.steps)
+            torch.cuda.synchronize()
+            dist.barrier()
+            red = torch.tensor([time.perf_counter() - tr, sum(q.stats()["segments"] for q in rs)],
+                               dtype=torch.float64, device=f"cuda:{local}")
+            r_break = rank_breakdown(dist, frames, world, torch.device("cuda", local))
+        finally:
+            for f in frames:
+                f.collective = collective
+        r_elapsed = torch.tensor([float(red[0])], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(r_elapsed, op=dist.ReduceOp.MAX)
+        r_seg = red[1:].clone()
+        dist.all_reduce(r_seg)
+        reduce_leg = {"value": round(float(r_seg.item()) / float(r_elapsed.item()) / 1e6, 3),
+                      "ms_per_step": round(float(r_elapsed.item()) / args.steps * 1000.0, 3),
+                      "collective_ms_per_launch_max_over_ranks":
+                          r_break.get("collective_ms_per_launch_max_over_ranks") if r_break else None,
+                      "render_ms_per_launch_max_over_ranks":
+                          r_break.get("render_ms_per_launch_max_over_ranks") if r_break else None}
+
     # The other tree on the same frames (N = 1): the reference's LBVH beside PT_BVH_SAH, or the other way round, timed
     # the same way (warm-up, K timed frames, one-frame-in-flight launches for the roofline), and one frame of each
     # compared bit for bit (the trees' closest hits differ only where the walk order decides them)
@@ -815,6 +855,8 @@ def main() -> int:
         line["config"]["image_matches_1gpu"] = matches_1gpu
         line["config"]["collective"] = {"backend": dist.get_backend(), "world_size": world,
                                         "frame_collective": frames[0].collective}
+        if reduce_leg is not None:
+            line["config"]["collective"]["reduce_leg"] = reduce_leg
         line["config"]["per_rank"] = breakdown
     if world == 1 and not args.no_cpu_baseline and args.workload in ("metric", "c1"):
         threads, why = host_threads(args.cpu_threads)

@@ -121,9 +121,11 @@ def _group_worker(rank, world, port, out_dir, collective):
         scene = _scene()
         cfg, _ = _setup()
         cams = [pt.camera(W, H, yaw=y, pitch=0.08, radius=12.5, center=(0, 1.2, 0)) for y in CAM_YAWS]
-        g = pt.FrameGroup(OracleFrameRenderer(scene), W, H, 3, dist, BAND, device="cpu", collective=collective)
+        # "gather8>reduce": bench.py's reduce leg, the live group switched from gather8 to the reduce between launches
+        first, then = collective.split(">") if ">" in collective else (collective, collective)
+        g = pt.FrameGroup(OracleFrameRenderer(scene), W, H, 3, dist, BAND, device="cpu", collective=first)
         def frames_of(n):
-            if collective != "gather8":
+            if g.collective != "gather8":
                 return [g.download(f) for f in range(n)]
             # gather8: rank 0 has every frame's 8-bit image after the launch; the float rows follow on demand
             img8 = [g.download(f)[1] for f in range(n)]
@@ -134,6 +136,7 @@ def _group_worker(rank, world, port, out_dir, collective):
         g.launch(cams, cfg, SPP)
         g.synchronize()
         full = frames_of(3)
+        g.collective = then
         g.launch(cams[1:], cfg, SPP)  # two frames: the stack's third frame is left as it was
         g.synchronize()
         two = frames_of(2)
@@ -146,7 +149,8 @@ def _group_worker(rank, world, port, out_dir, collective):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world,collective", [(2, "gather"), (3, "gather"), (2, "reduce"), (1, "gather"),
-                                              (1, "reduce"), (2, "gather8"), (3, "gather8"), (1, "gather8")])
+                                              (1, "reduce"), (2, "gather8"), (3, "gather8"), (1, "gather8"),
+                                              (3, "gather8>reduce")])
 def test_frame_group_equals_single_renders(tmp_path, world, collective):
     """World size 1 is bench.py --rccl's path: a one-rank group still takes the collective (band count 1, the
     gather's own piece placed, or the reduce of the one buffer)."""

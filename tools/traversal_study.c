@@ -28,11 +28,11 @@ typedef struct { int n; int* left; int* right; sn* oct[8]; const pt_bvh_node_dev
 
 #define MAXM 16
 static smesh g_mesh[MAXM];
-static unsigned long long g_stat[16];
+static unsigned long long g_stat[20];
 static unsigned long long g_mesh_tris[MAXM], g_mesh_nodes[MAXM], g_mesh_calls[MAXM], g_mesh_oct[MAXM], g_mesh_n[MAXM],
-    g_mesh_steps[MAXM];
+    g_mesh_steps[MAXM], g_mesh_skip[MAXM], g_mesh_skip1[MAXM], g_mesh_leafskip[MAXM];
 enum { S_CALLS, S_REF_NODES, S_OCT_NODES, S_OCTM_NODES, S_STACK_BOX, S_STACK_POPS, S_OCT_MISMATCH, S_OCTM_MISMATCH,
-       S_ANOM, S_TIE, S_STACK_MISMATCH, S_REF_HITS, S_REF_STEPS, S_CHAIN_STEPS, S_CHAIN_LEN, S_NSTAT };
+       S_ANOM, S_TIE, S_STACK_MISMATCH, S_REF_HITS, S_REF_STEPS, S_CHAIN_STEPS, S_CHAIN_LEN, S_SKIP_STEPS, S_SKIP1_STEPS, S_LEAFSKIP_STEPS, S_NSTAT };
 
 static void cen(const pt_bounding_box* b, float c[3]) {
     c[0] = 0.5f * (b->left_bottom.x + b->right_top.x);
@@ -175,6 +175,13 @@ static void walk_stack(const or_scene* sc, const smesh* s, or_v3 o, or_v3 d, or_
     }
 }
 
+static int box_pass(const pt_bounding_box* bb, or_v3 o, or_v3 inv, float bt) {
+    float lo[3] = {bb->left_bottom.x, bb->left_bottom.y, bb->left_bottom.z};
+    float hi[3] = {bb->right_top.x, bb->right_top.y, bb->right_top.z};
+    float e;
+    return sbox(lo, hi, o, inv, &e) && e <= bt;
+}
+
 static void study_hook(const void* scv, int m, float ox, float oy, float oz, float dx, float dy, float dz, int hit,
                        float t, int tri) {
     const or_scene* sc = (const or_scene*)scv;
@@ -282,6 +289,88 @@ static void study_hook(const void* scv, int m, float ox, float oy, float oz, flo
             else pos = nd[q].is_leaf ? q : q + 1;
         }
     }
+    /* skip speculation: every record also carries the box of its skip target (and that target's own skip index), so
+       a step at pos tests pos; when pos fails, skip(pos) in the same step; when pos passes (internal), pos + 1 and, if
+       that fails, skip(pos + 1) (carried by pos + 1's record). The same visits in the same order as the reference's
+       walk; a passing leaf met as a speculated record is re-tested with its triangle next step. */
+    {
+        const pt_bvh_node_device* nd = s->ref;
+        float bt = INFINITY;
+        int pos = 0;
+#define PASSES(i) ((i) < s->n && box_pass(&nd[i].box, o, inv, bt))
+        while (pos != s->n) {
+            loc[S_SKIP_STEPS]++;
+            if (!PASSES(pos)) {
+                const int sk = nd[pos].next_node_index;
+                if (sk == s->n) { pos = sk; continue; }
+                if (PASSES(sk)) pos = nd[sk].is_leaf ? sk : sk + 1;
+                else pos = nd[sk].next_node_index;
+                continue;
+            }
+            if (nd[pos].is_leaf) {
+                float tt, t1, t2;
+                int ti2 = nd[pos].triangle_indices[0];
+                if (triangle_intersect(&sc->tris[ti2], o, d, &tt, &t1, &t2) && tt > 0.0f && tt < bt) bt = tt;
+                pos++;
+                continue;
+            }
+            const int q = pos + 1;
+            if (PASSES(q)) { pos = nd[q].is_leaf ? q : q + 1; continue; }
+            const int sk = nd[q].next_node_index;
+            if (sk == s->n) { pos = sk; continue; }
+            if (PASSES(sk)) pos = nd[sk].is_leaf ? sk : sk + 1;
+            else pos = nd[sk].next_node_index;
+        }
+        /* skip1: the same without skip(pos + 1): a failing pos + 1 moves the walk to its skip target untested (one
+           speculated box per step: pos + 1's when pos passes, skip(pos)'s when it fails) */
+        bt = INFINITY;
+        pos = 0;
+        while (pos != s->n) {
+            loc[S_SKIP1_STEPS]++;
+            if (!PASSES(pos)) {
+                const int sk = nd[pos].next_node_index;
+                if (sk == s->n) { pos = sk; continue; }
+                if (PASSES(sk)) pos = nd[sk].is_leaf ? sk : sk + 1;
+                else pos = nd[sk].next_node_index;
+                continue;
+            }
+            if (nd[pos].is_leaf) {
+                float tt, t1, t2;
+                int ti2 = nd[pos].triangle_indices[0];
+                if (triangle_intersect(&sc->tris[ti2], o, d, &tt, &t1, &t2) && tt > 0.0f && tt < bt) bt = tt;
+                pos++;
+                continue;
+            }
+            const int q = pos + 1;
+            if (PASSES(q)) pos = nd[q].is_leaf ? q : q + 1;
+            else pos = nd[q].next_node_index;
+        }
+        /* leafskip: the present layout (a leaf's skip target is the record after its triangle) with 96 B per step: a
+           failing leaf's successor is tested in the same step; nothing else changes */
+        bt = INFINITY;
+        pos = 0;
+        while (pos != s->n) {
+            loc[S_LEAFSKIP_STEPS]++;
+            if (!PASSES(pos)) {
+                const int sk = nd[pos].next_node_index;
+                if (!nd[pos].is_leaf || sk == s->n) { pos = sk; continue; }
+                if (PASSES(sk)) pos = nd[sk].is_leaf ? sk : sk + 1;
+                else pos = nd[sk].next_node_index;
+                continue;
+            }
+            if (nd[pos].is_leaf) {
+                float tt, t1, t2;
+                int ti2 = nd[pos].triangle_indices[0];
+                if (triangle_intersect(&sc->tris[ti2], o, d, &tt, &t1, &t2) && tt > 0.0f && tt < bt) bt = tt;
+                pos++;
+                continue;
+            }
+            const int q = pos + 1;
+            if (PASSES(q)) pos = nd[q].is_leaf ? q : q + 1;
+            else pos = nd[q].next_node_index;
+        }
+#undef PASSES
+    }
     best_t b;
     walk_oct(sc, s, k, o, d, inv, 1.0f, &b, &loc[S_OCT_NODES], &loc[S_ANOM], &loc[S_TIE]);
     int same = hit ? (b.tri == tri && b.t == t) : (b.tri < 0);
@@ -297,6 +386,9 @@ static void study_hook(const void* scv, int m, float ox, float oy, float oz, flo
     __atomic_fetch_add(&g_mesh_nodes[m], loc[S_REF_NODES], __ATOMIC_RELAXED);
     __atomic_fetch_add(&g_mesh_oct[m], loc[S_OCT_NODES], __ATOMIC_RELAXED);
     __atomic_fetch_add(&g_mesh_steps[m], loc[S_REF_STEPS], __ATOMIC_RELAXED);
+    __atomic_fetch_add(&g_mesh_skip[m], loc[S_SKIP_STEPS], __ATOMIC_RELAXED);
+    __atomic_fetch_add(&g_mesh_skip1[m], loc[S_SKIP1_STEPS], __ATOMIC_RELAXED);
+    __atomic_fetch_add(&g_mesh_leafskip[m], loc[S_LEAFSKIP_STEPS], __ATOMIC_RELAXED);
     __atomic_fetch_add(&g_mesh_calls[m], 1, __ATOMIC_RELAXED);
     g_mesh_n[m] = s->n;
 }
@@ -342,9 +434,12 @@ void study_stats(unsigned long long* out) {
     for (int i = 0; i < S_NSTAT; i++) out[i] = g_stat[i];
     for (int m = 0; m < MAXM; m++)
         if (g_mesh_calls[m])
-            printf("  mesh %d: %llu nodes, %llu walks, ref nodes/walk %.2f, steps/walk %.2f, tris/walk %.2f, oct nodes/walk %.2f\n",
+            printf("  mesh %d: %llu nodes, %llu walks, ref nodes/walk %.2f, steps/walk %.2f, skip-spec steps/walk %.2f (one box: %.2f, leaves only: %.2f), "
+                   "tris/walk %.2f, oct nodes/walk %.2f\n",
                    m, g_mesh_n[m], g_mesh_calls[m], (double)g_mesh_nodes[m] / g_mesh_calls[m],
-                   (double)g_mesh_steps[m] / g_mesh_calls[m], (double)g_mesh_tris[m] / g_mesh_calls[m],
+                   (double)g_mesh_steps[m] / g_mesh_calls[m], (double)g_mesh_skip[m] / g_mesh_calls[m],
+                   (double)g_mesh_skip1[m] / g_mesh_calls[m], (double)g_mesh_leafskip[m] / g_mesh_calls[m],
+                   (double)g_mesh_tris[m] / g_mesh_calls[m],
                    (double)g_mesh_oct[m] / g_mesh_calls[m]);
     fflush(stdout);
 }

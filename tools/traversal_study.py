@@ -21,7 +21,9 @@ import oracle  # noqa: E402
 import pathtracerwithcuda_amd as pt  # noqa: E402
 
 NAMES = ["calls", "ref_nodes", "oct_nodes", "octm_nodes", "stack_boxes", "stack_pops", "oct_mismatch",
-         "octm_mismatch", "anomalies", "ties", "stack_mismatch", "ref_hits", "ref_steps", "chain_steps", "chain_len"]
+         "octm_mismatch", "anomalies", "ties", "stack_mismatch", "ref_hits", "ref_steps", "chain_steps", "chain_len",
+         "skip_spec_steps", "skip_spec1_steps",
+         "leaf_skip_steps"]
 
 
 def main():
@@ -46,7 +48,7 @@ def main():
     pix = np.sort(rng.choice(wl.width * wl.height, size=sample, replace=False)).astype(np.int32)
     t0 = time.time()
     oracle.render(scene.view, cam, cfg, 1, passes, pixels=pix, with_u8=False)
-    st = (C.c_ulonglong * 16)()
+    st = (C.c_ulonglong * 20)()
     L.study_stats(st)
     d = dict(zip(NAMES, list(st)[:len(NAMES)]))
     c = max(d["calls"], 1)
