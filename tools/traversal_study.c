@@ -24,7 +24,8 @@ static void study_hook(const void* sc, int m, float ox, float oy, float oz, floa
 #include "../oracle/oracle.c"
 
 typedef struct { float lo[3], hi[3]; int skip, tri, orig; } sn;
-typedef struct { int n; int* left; int* right; sn* oct[8]; const pt_bvh_node_device* ref; unsigned long long* visits; } smesh;
+typedef struct { int n; int* left; int* right; sn* oct[8]; const pt_bvh_node_device* ref; unsigned long long* visits;
+                 unsigned long long* passes; sn* meas; } smesh;
 
 #define MAXM 16
 static smesh g_mesh[MAXM];
@@ -32,7 +33,7 @@ static unsigned long long g_stat[20];
 static unsigned long long g_mesh_tris[MAXM], g_mesh_nodes[MAXM], g_mesh_calls[MAXM], g_mesh_oct[MAXM], g_mesh_n[MAXM],
     g_mesh_steps[MAXM], g_mesh_skip[MAXM], g_mesh_skip1[MAXM], g_mesh_leafskip[MAXM];
 enum { S_CALLS, S_REF_NODES, S_OCT_NODES, S_OCTM_NODES, S_STACK_BOX, S_STACK_POPS, S_OCT_MISMATCH, S_OCTM_MISMATCH,
-       S_ANOM, S_TIE, S_STACK_MISMATCH, S_REF_HITS, S_REF_STEPS, S_CHAIN_STEPS, S_CHAIN_LEN, S_SKIP_STEPS, S_SKIP1_STEPS, S_LEAFSKIP_STEPS, S_NSTAT };
+       S_ANOM, S_TIE, S_STACK_MISMATCH, S_REF_HITS, S_REF_STEPS, S_CHAIN_STEPS, S_CHAIN_LEN, S_SKIP_STEPS, S_SKIP1_STEPS, S_LEAFSKIP_STEPS, S_MEAS_STEPS, S_NSTAT };
 
 static void cen(const pt_bounding_box* b, float c[3]) {
     c[0] = 0.5f * (b->left_bottom.x + b->right_top.x);
@@ -80,6 +81,7 @@ static void prepare(const or_scene* sc, int m) {
     s->left = malloc(sizeof(int) * n);
     s->right = malloc(sizeof(int) * n);
     s->visits = calloc(n, sizeof(unsigned long long));
+    s->passes = calloc(n, sizeof(unsigned long long));
     for (int p = 0; p < n; p++) {
         if (nodes[p].is_leaf) { s->left[p] = s->right[p] = -1; continue; }
         s->left[p] = p + 1;
@@ -211,6 +213,7 @@ static void study_hook(const void* scv, int m, float ox, float oy, float oz, flo
             loc[S_REF_NODES]++;
             __atomic_fetch_add(&s->visits[pos], 1, __ATOMIC_RELAXED);
             if (sbox(lo, hi, o, inv, &e) && e <= b.t) {
+                __atomic_fetch_add(&s->passes[pos], 1, __ATOMIC_RELAXED);
                 if (nd[pos].is_leaf) {
                     float tt, t1, t2;
                     __atomic_fetch_add(&g_mesh_tris[m], 1, __ATOMIC_RELAXED);
@@ -371,6 +374,24 @@ static void study_hook(const void* scv, int m, float ox, float oy, float oz, flo
         }
 #undef PASSES
     }
+    if (s->meas) {  /* the GPU two-record step over the measured-order copy (study_reorder) */
+        const sn* a = s->meas;
+        float bt = INFINITY, e;
+        int pos = 0;
+        while (pos != s->n) {
+            loc[S_MEAS_STEPS]++;
+            if (!(sbox(a[pos].lo, a[pos].hi, o, inv, &e) && e <= bt)) { pos = a[pos].skip; continue; }
+            if (a[pos].tri >= 0) {
+                float tt, t1, t2;
+                if (triangle_intersect(&sc->tris[a[pos].tri], o, d, &tt, &t1, &t2) && tt > 0.0f && tt < bt) bt = tt;
+                pos++;
+                continue;
+            }
+            const int q = pos + 1;
+            if (!(sbox(a[q].lo, a[q].hi, o, inv, &e) && e <= bt)) pos = a[q].skip;
+            else pos = a[q].tri >= 0 ? q : q + 1;
+        }
+    }
     best_t b;
     walk_oct(sc, s, k, o, d, inv, 1.0f, &b, &loc[S_OCT_NODES], &loc[S_ANOM], &loc[S_TIE]);
     int same = hit ? (b.tri == tri && b.t == t) : (b.tri < 0);
@@ -426,6 +447,59 @@ static void coverage(smesh* s, int budget) {
     printf("    budget %5d: SA-greedy %d nodes cover %.3f of visits; BFS %d nodes cover %.3f\n", budget, cnt,
            (double)cov / tot, c2, (double)cov2 / tot);
     free(in); free(in2); free(q);
+}
+
+/* study_reorder: each mesh's children re-ordered by the expected GPU steps (pt_sah_order_by_steps' recurrence) under the
+   MEASURED pass probabilities of the sample rendered so far (passes[child] / passes[parent]), into s->meas; the next
+   render's walks are counted over it (S_MEAS_STEPS). mode 1: measured probabilities, 0: the surface-area ratio
+   (the shipped order 6 recomputed, a check). */
+static double *g_start, *g_free;
+static double sa(const pt_bounding_box* b);
+/* start(Y) = 1 + P(Y)(free(F) + start(S)), free(Y) = P(Y)(start(F) + start(S)); leaf: start 1, free P */
+static void dp(smesh* s, int p, double P, int mode) {
+    if (s->left[p] < 0) { g_start[p] = 1.0; g_free[p] = P; return; }
+    int c[2] = {s->left[p], s->right[p]};
+    for (int i = 0; i < 2; i++) {
+        double pr;
+        if (mode == 1) pr = s->passes[p] ? (double)s->passes[c[i]] / (double)s->passes[p] : 0.0;
+        else {
+            const pt_bounding_box* cb = &s->ref[c[i]].box;
+            int thin = cb->left_bottom.x == cb->right_top.x || cb->left_bottom.y == cb->right_top.y ||
+                       cb->left_bottom.z == cb->right_top.z;
+            double sp = sa(&s->ref[p].box);
+            pr = (s->left[c[i]] < 0 && thin) || !(sp > 0.0) ? 1.0 : fmin(1.0, sa(cb) / sp);
+        }
+        dp(s, c[i], pr > 1.0 ? 1.0 : pr, mode);
+    }
+    double a = g_free[c[0]] + g_start[c[1]], b = g_free[c[1]] + g_start[c[0]];
+    if (b < a) { s->left[p] = c[1]; s->right[p] = c[0]; a = b; }
+    g_start[p] = 1.0 + P * a;
+    g_free[p] = P * (g_start[c[0]] + g_start[c[1]]);
+}
+static int emit_meas(smesh* s, int p, int out) {
+    const pt_bvh_node_device* nd = &s->ref[p];
+    sn* e = &s->meas[out];
+    e->lo[0] = nd->box.left_bottom.x; e->lo[1] = nd->box.left_bottom.y; e->lo[2] = nd->box.left_bottom.z;
+    e->hi[0] = nd->box.right_top.x; e->hi[1] = nd->box.right_top.y; e->hi[2] = nd->box.right_top.z;
+    e->orig = p;
+    if (s->left[p] < 0) { e->tri = nd->triangle_indices[0]; e->skip = out + 1; return out + 1; }
+    e->tri = -1;
+    int nx = emit_meas(s, s->left[p], out + 1);
+    nx = emit_meas(s, s->right[p], nx);
+    e->skip = nx;
+    return nx;
+}
+void study_reorder(int mode) {
+    for (int m = 0; m < MAXM; m++) {
+        smesh* s = &g_mesh[m];
+        if (!s->n) continue;
+        g_start = calloc(s->n, sizeof(double));
+        g_free = calloc(s->n, sizeof(double));
+        dp(s, 0, 1.0, mode);
+        s->meas = malloc(sizeof(sn) * s->n);
+        if (emit_meas(s, 0, 0) != s->n) abort();
+        free(g_start); free(g_free);
+    }
 }
 
 void study_stats(unsigned long long* out) {

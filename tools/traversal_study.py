@@ -23,7 +23,7 @@ import pathtracerwithcuda_amd as pt  # noqa: E402
 NAMES = ["calls", "ref_nodes", "oct_nodes", "octm_nodes", "stack_boxes", "stack_pops", "oct_mismatch",
          "octm_mismatch", "anomalies", "ties", "stack_mismatch", "ref_hits", "ref_steps", "chain_steps", "chain_len",
          "skip_spec_steps", "skip_spec1_steps",
-         "leaf_skip_steps"]
+         "leaf_skip_steps", "measured_order_steps"]
 
 
 def main():
@@ -51,6 +51,19 @@ def main():
     st = (C.c_ulonglong * 20)()
     L.study_stats(st)
     d = dict(zip(NAMES, list(st)[:len(NAMES)]))
+    reorder = os.environ.get("STUDY_REORDER")  # 1: child order from the sample's measured pass rates, 0: surface area
+    if reorder is not None:
+        # the re-ordered trees are walked on a second, disjoint pixel sample (the first one trained them)
+        L.study_reorder(int(reorder))
+        rest = np.setdiff1d(np.arange(wl.width * wl.height), pix)
+        pix2 = np.sort(np.random.default_rng(2).choice(rest, size=sample, replace=False)).astype(np.int32)
+        oracle.render(scene.view, cam, cfg, 1, passes, pixels=pix2, with_u8=False)
+        st2 = (C.c_ulonglong * 20)()
+        L.study_stats(st2)
+        d2 = {k: b - a for k, a, b in zip(NAMES, list(st)[:len(NAMES)], list(st2)[:len(NAMES)])}
+        c2 = max(d2["calls"], 1)
+        print(f"second sample: reference-order steps per walk {d2['ref_steps'] / c2:.3f}, re-ordered "
+              f"({'measured' if reorder == '1' else 'surface area'}) {d2['measured_order_steps'] / c2:.3f}")
     c = max(d["calls"], 1)
     print(f"{sample} px x {passes} passes, {time.time() - t0:.1f} s")
     for k, v in d.items():
