@@ -16,6 +16,7 @@
  */
 #include <stdint.h>
 #include <stdio.h>
+#include <string.h>
 
 struct or_scene_fwd;
 static void study_hook(const void* sc, int m, float ox, float oy, float oz, float dx, float dy, float dz, int hit,
@@ -31,9 +32,9 @@ typedef struct { int n; int* left; int* right; sn* oct[8]; const pt_bvh_node_dev
 static smesh g_mesh[MAXM];
 static unsigned long long g_stat[20];
 static unsigned long long g_mesh_tris[MAXM], g_mesh_nodes[MAXM], g_mesh_calls[MAXM], g_mesh_oct[MAXM], g_mesh_n[MAXM],
-    g_mesh_steps[MAXM], g_mesh_skip[MAXM], g_mesh_skip1[MAXM], g_mesh_leafskip[MAXM];
+    g_mesh_steps[MAXM], g_mesh_skip[MAXM], g_mesh_skip1[MAXM], g_mesh_leafskip[MAXM], g_mesh_pair[MAXM];
 enum { S_CALLS, S_REF_NODES, S_OCT_NODES, S_OCTM_NODES, S_STACK_BOX, S_STACK_POPS, S_OCT_MISMATCH, S_OCTM_MISMATCH,
-       S_ANOM, S_TIE, S_STACK_MISMATCH, S_REF_HITS, S_REF_STEPS, S_CHAIN_STEPS, S_CHAIN_LEN, S_SKIP_STEPS, S_SKIP1_STEPS, S_LEAFSKIP_STEPS, S_MEAS_STEPS, S_NSTAT };
+       S_ANOM, S_TIE, S_STACK_MISMATCH, S_REF_HITS, S_REF_STEPS, S_CHAIN_STEPS, S_CHAIN_LEN, S_SKIP_STEPS, S_SKIP1_STEPS, S_LEAFSKIP_STEPS, S_MEAS_STEPS, S_PAIR_STEPS, S_NSTAT };
 
 static void cen(const pt_bounding_box* b, float c[3]) {
     c[0] = 0.5f * (b->left_bottom.x + b->right_top.x);
@@ -374,6 +375,39 @@ static void study_hook(const void* scv, int m, float ox, float oy, float oz, flo
         }
 #undef PASSES
     }
+    /* pair merge: an internal node P whose children are two leaves, the first with P's own box (bit for bit: a thin
+       leaf widened to its parent's), is dropped from the layout; its first leaf carries P's test (same box, same
+       min_t) and a failing test skips both leaves. The GPU two-record step otherwise as ref_steps. */
+    {
+        const pt_bvh_node_device* nd = s->ref;
+#define MERGED(i) ((i) + 2 < s->n && !nd[i].is_leaf && nd[(i) + 1].is_leaf && nd[(i) + 2].is_leaf && \
+                   nd[i].next_node_index == (i) + 3 && !memcmp(&nd[i].box, &nd[(i) + 1].box, sizeof(pt_bounding_box)))
+        float bt = INFINITY;
+        int pos = 0;
+        while (pos != s->n) {
+            loc[S_PAIR_STEPS]++;
+            float e;
+            if (MERGED(pos)) pos++;  /* the walk stands on the merged leaf (P's record does not exist) */
+            if (!box_pass(&nd[pos].box, o, inv, bt)) {
+                pos = (pos > 0 && nd[pos].is_leaf && MERGED(pos - 1)) ? pos + 2 : nd[pos].next_node_index;
+                continue;
+            }
+            if (nd[pos].is_leaf) {
+                float tt, t1, t2;
+                int ti2 = nd[pos].triangle_indices[0];
+                if (triangle_intersect(&sc->tris[ti2], o, d, &tt, &t1, &t2) && tt > 0.0f && tt < bt) bt = tt;
+                pos++;
+                continue;
+            }
+            int q = pos + 1;
+            int qm = MERGED(q);
+            if (qm) q++;
+            if (!box_pass(&nd[q].box, o, inv, bt)) pos = qm ? q + 2 : nd[q].next_node_index;
+            else pos = nd[q].is_leaf ? q : q + 1;
+            (void)e;
+        }
+#undef MERGED
+    }
     if (s->meas) {  /* the GPU two-record step over the measured-order copy (study_reorder) */
         const sn* a = s->meas;
         float bt = INFINITY, e;
@@ -410,6 +444,7 @@ static void study_hook(const void* scv, int m, float ox, float oy, float oz, flo
     __atomic_fetch_add(&g_mesh_skip[m], loc[S_SKIP_STEPS], __ATOMIC_RELAXED);
     __atomic_fetch_add(&g_mesh_skip1[m], loc[S_SKIP1_STEPS], __ATOMIC_RELAXED);
     __atomic_fetch_add(&g_mesh_leafskip[m], loc[S_LEAFSKIP_STEPS], __ATOMIC_RELAXED);
+    __atomic_fetch_add(&g_mesh_pair[m], loc[S_PAIR_STEPS], __ATOMIC_RELAXED);
     __atomic_fetch_add(&g_mesh_calls[m], 1, __ATOMIC_RELAXED);
     g_mesh_n[m] = s->n;
 }
@@ -508,11 +543,12 @@ void study_stats(unsigned long long* out) {
     for (int i = 0; i < S_NSTAT; i++) out[i] = g_stat[i];
     for (int m = 0; m < MAXM; m++)
         if (g_mesh_calls[m])
-            printf("  mesh %d: %llu nodes, %llu walks, ref nodes/walk %.2f, steps/walk %.2f, skip-spec steps/walk %.2f (one box: %.2f, leaves only: %.2f), "
+            printf("  mesh %d: %llu nodes, %llu walks, ref nodes/walk %.2f, steps/walk %.2f, skip-spec steps/walk %.2f (one box: %.2f, leaves only: %.2f), pair-merged steps/walk %.2f, "
                    "tris/walk %.2f, oct nodes/walk %.2f\n",
                    m, g_mesh_n[m], g_mesh_calls[m], (double)g_mesh_nodes[m] / g_mesh_calls[m],
                    (double)g_mesh_steps[m] / g_mesh_calls[m], (double)g_mesh_skip[m] / g_mesh_calls[m],
                    (double)g_mesh_skip1[m] / g_mesh_calls[m], (double)g_mesh_leafskip[m] / g_mesh_calls[m],
+                   (double)g_mesh_pair[m] / g_mesh_calls[m],
                    (double)g_mesh_tris[m] / g_mesh_calls[m],
                    (double)g_mesh_oct[m] / g_mesh_calls[m]);
     fflush(stdout);

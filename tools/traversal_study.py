@@ -23,7 +23,8 @@ import pathtracerwithcuda_amd as pt  # noqa: E402
 NAMES = ["calls", "ref_nodes", "oct_nodes", "octm_nodes", "stack_boxes", "stack_pops", "oct_mismatch",
          "octm_mismatch", "anomalies", "ties", "stack_mismatch", "ref_hits", "ref_steps", "chain_steps", "chain_len",
          "skip_spec_steps", "skip_spec1_steps",
-         "leaf_skip_steps", "measured_order_steps"]
+         "leaf_skip_steps", "measured_order_steps",
+         "pair_merged_steps"]
 
 
 def main():
