@@ -291,7 +291,11 @@ def lib() -> C.CDLL:
         from .build import build
         build()
     handle = C.CDLL(LIB, mode=C.RTLD_GLOBAL)
+    # PT_ABI_OLD_LIB=1: an earlier round's library loaded for an A/B (PT_LIBDIR); exports it predates are skipped
+    lenient = os.environ.get("PT_ABI_OLD_LIB") == "1"
     for name, (res, args) in _PROTOS.items():
+        if lenient and not hasattr(handle, name):
+            continue
         fn = getattr(handle, name)  # AttributeError = missing export: fail loudly
         fn.restype = res
         fn.argtypes = args
