@@ -551,7 +551,8 @@ struct pt_context {
     LaunchParams* spec_params[2] = {nullptr, nullptr};  // each slot's launch parameters (device)
     hipEvent_t spec_done[2] = {nullptr, nullptr};
     hipStream_t acc_stream = nullptr;  // the ABI's per-call accumulate and download
-    hipEvent_t chunk_up[4] = {nullptr, nullptr, nullptr, nullptr};  // the running sum's upload, per chunk
+    // the running sum's upload, per chunk; [4]: the call's last accumulate (the result's digest waits for it)
+    hipEvent_t chunk_up[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     // the reference ABI on host-visible images: a continuation call's copy of the caller's running sum (kept apart
     // from the result, so the call can be redone on an edited scene) and digests (launch_digest_words) of the sum a
     // call received ([0]) and returned ([1]). A received sum that is not the one the last call returned means that
@@ -1341,26 +1342,32 @@ int abi_render_pass(pt_context* ctx, const pt_render_camera* cam, const pt_confi
     PT_HIP(hipMemcpyAsync(ctx->params, &lp, sizeof(lp), hipMemcpyHostToDevice, as));
     const int K = io.direct || io.pageable ? 1 : 4;
     const bool up = !io.direct && pass != 1;  // pass 1 overwrites: nothing to add into
-    // the caller's running sum lands in caller_sum (the accumulate reads it there) and is digested as it arrives;
-    // the result is digested before it goes down (sum_digest, path_tracer_kernel)
+    // the caller's running sum lands in caller_sum (the accumulate reads it there); the sum received and the result
+    // are each digested once, on copy_stream, beside the chunks' copies (sum_digest, path_tracer_kernel): after the
+    // last chunk's upload, and once the last accumulate is done, while the last chunks go down (one digest launch per
+    // chunk and stream, in line with the copies, cost ~0.1 ms per call)
     if (up) PT_HIP(hipMemsetAsync(ctx->sum_digest, 0, sizeof(unsigned long long), ctx->copy_stream));
-    if (!io.direct) PT_HIP(hipMemsetAsync(ctx->sum_digest + 1, 0, sizeof(unsigned long long), as));
+    if (!io.direct) PT_HIP(hipMemsetAsync(ctx->sum_digest + 1, 0, sizeof(unsigned long long), ctx->copy_stream));
     for (int c = 0; c < K; c++) {
         const int b0 = (int)((long long)units * c / K), b1 = (int)((long long)units * (c + 1) / K);
         if (up) {
             PT_HIP(hipMemcpyAsync(ctx->caller_sum + (size_t)b0 * 3, io.img + b0, (size_t)(b1 - b0) * 12,
                                   hipMemcpyDefault, ctx->copy_stream));
-            PT_HIP(launch_digest_words(ctx->caller_sum, (size_t)b0 * 3, (size_t)b1 * 3, ctx->sum_digest, ctx->copy_stream));
             PT_HIP(hipEventRecord(ctx->chunk_up[c], ctx->copy_stream));
             PT_HIP(hipStreamWaitEvent(as, ctx->chunk_up[c], 0));
         }
         PT_HIP(launch_accumulate_one(ctx->params, b0, b1, pass, ctx->spec_lg, pass - ctx->spec_first[slot], 1,
                                      ctx->spec_rad[slot], up ? ctx->caller_sum : nullptr, as));
         if (!io.direct) {
-            PT_HIP(launch_digest_words(ctx->image, (size_t)b0 * 3, (size_t)b1 * 3, ctx->sum_digest + 1, as));
+            if (c == K - 1) PT_HIP(hipEventRecord(ctx->chunk_up[4], as));
             PT_HIP(hipMemcpyAsync(io.img + b0, ctx->image + (size_t)b0 * 3, (size_t)(b1 - b0) * 12, hipMemcpyDefault, as));
             PT_HIP(hipMemcpyAsync(io.img8 + b0, ctx->image256 + (size_t)b0 * 3, (size_t)(b1 - b0) * 3, hipMemcpyDefault, as));
         }
+    }
+    if (up) PT_HIP(launch_digest_words(ctx->caller_sum, 0, (size_t)units * 3, ctx->sum_digest, ctx->copy_stream));
+    if (!io.direct) {
+        PT_HIP(hipStreamWaitEvent(ctx->copy_stream, ctx->chunk_up[4], 0));
+        PT_HIP(launch_digest_words(ctx->image, 0, (size_t)units * 3, ctx->sum_digest + 1, ctx->copy_stream));
     }
     *downloaded = !io.direct;
     *done = as;
