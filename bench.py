@@ -543,6 +543,7 @@ def main() -> int:
     # compares them bitwise (float running sum and 8-bit image); the line carries config.image_matches_1gpu and a
     # mismatch exits 3
     matches_1gpu = None
+    solo_frame = None
     watch.stage("self-check")
     if distributed and group > 1:
         # "gather8": the float rows of the last timed launch's frames to rank 0 for the check (every rank)
@@ -562,6 +563,8 @@ def main() -> int:
             for f, (tiled, tiled8) in zip(picks, got):
                 solo.render(cams[f], cfg, 1, spp, write_u8=2)
                 one, one8 = solo.download()
+                if f == 0:
+                    solo_frame = (one, one8)  # also the reference for the reduce leg's frames (one camera)
                 matches_1gpu &= bool(np.array_equal(tiled.view(np.uint32).reshape(-1), one.view(np.uint32).reshape(-1))
                                      and np.array_equal(tiled8.reshape(-1), one8.reshape(-1)))
         finally:
@@ -620,6 +623,13 @@ def main() -> int:
             red = torch.tensor([time.perf_counter() - tr, sum(q.stats()["segments"] for q in rs)],
                                dtype=torch.float64, device=f"cuda:{local}")
             r_break = rank_breakdown(dist, frames, world, torch.device("cuda", local))
+            # rank 0 holds the reduced frames: the last launch's first frame must be the 1-GPU frame too (one camera
+            # for every frame unless --orbit)
+            reduce_matches = None
+            if rank == 0 and solo_frame is not None and not args.orbit:
+                got_f, got_8 = frames[last_launch[0]].download(0)
+                reduce_matches = bool(np.array_equal(got_f.view(np.uint32).reshape(-1), solo_frame[0].view(np.uint32).reshape(-1))
+                                      and np.array_equal(got_8.reshape(-1), solo_frame[1].reshape(-1)))
         finally:
             for f in frames:
                 f.collective = collective
@@ -632,7 +642,10 @@ def main() -> int:
                       "collective_ms_per_launch_max_over_ranks":
                           r_break.get("collective_ms_per_launch_max_over_ranks") if r_break else None,
                       "render_ms_per_launch_max_over_ranks":
-                          r_break.get("render_ms_per_launch_max_over_ranks") if r_break else None}
+                          r_break.get("render_ms_per_launch_max_over_ranks") if r_break else None,
+                      "image_matches_1gpu": reduce_matches}
+        if reduce_matches is False:
+            matches_1gpu = False  # the line says so and the run exits 3
 
     # The other tree on the same frames (N = 1): the reference's LBVH beside PT_BVH_SAH, or the other way round, timed
     # the same way (warm-up, K timed frames, one-frame-in-flight launches for the roofline), and one frame of each
