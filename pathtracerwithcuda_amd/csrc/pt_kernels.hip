@@ -1108,12 +1108,14 @@ hipError_t launch_pass(const LaunchParams* params_dev, const PassChoice& pc, int
         // fused multiply-adds made the triangle test cheaper: +0.3 % over four rounds, profiles/r04/knobs/)
         // (the generation ring holds one chunk: 1..64 units)
         static const int chunk = env_int("PT_CHUNK_MEGA", 64, 1, PT_RING);
-        // the shading batch waits for 40 ready lanes with a medium walked exactly (the medium step makes a batch
-        // dearer: C4 5952-5966 vs 5747 Mrays/s, 36: 5936-5952, 44: 5814, profiles/r04/knobs/c4_c5_shade_min.txt),
-        // 28 otherwise (C5 at 32 / 36: ±0 / -1 %; the medium-bounded walk, shorter: 9450 at 40 vs 9573-9597)
+        // the shading batch waits for 32 ready lanes with a medium walked exactly (the medium step makes a batch
+        // dearer; round 4 on the reference tree: 40, C4 5952-5966 vs 5747 Mrays/s at 28, profiles/r04/knobs/
+        // c4_c5_shade_min.txt; round 6 on the SAH tree, whose walks are shorter: 32 7955-7975 vs 7813-7839 at 40,
+        // 24 / 28 / 36 7876-7954, 48 7134-7150, profiles/r06/knobs/c4_shade_min.txt), 28 otherwise (C5 at 32 / 36:
+        // ±0 / -1 %; the medium-bounded walk, shorter: 9450 at 40 vs 9573-9597)
         static const int shade_env = env_int("PT_SHADE_MIN", 0, 0, 64);
         const bool dear = (pc.feat & PT_FEAT_MEDIUM) && !(pc.feat & PT_FEAT_MBOUND);
-        const int shade_min = shade_env ? shade_env : dear ? 40 : 28;
+        const int shade_min = shade_env ? shade_env : dear ? 32 : 28;
         static const int walk_steps = env_int("PT_WALK_STEPS", 7, 1, 64);
         static const int tri_min = env_int("PT_TRI_MIN", 4, 1, 64);
         static const int walk_min = env_int("PT_WALK_MIN", 8, 0, 64);
