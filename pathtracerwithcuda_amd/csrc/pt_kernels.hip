@@ -974,8 +974,10 @@ static PassFn pass_fn(bool leaf1, bool stats, int minw) {
 // 8 when the scene reaches neither textures nor a participating medium (64 VGPRs without spills since round 4
 // recomputes the hit point and the clamp bound where they are used: metric +1.6 % with frame groups, +1.2 %
 // without, C3 +1.1 %, C2 +0.9 %; profiles/r04/knobs/waves_ab2.txt), 7 with textures (72 VGPRs, one cold
-// spill; +6.7 % over 6 on C5) and 6 with a medium (80 VGPRs; 7 fits without spills since round 4 but is slower:
-// C4 5567-5573 vs 5709-5731 Mrays/s, profiles/r04/knobs/waves_ab1.txt).
+// spill; +6.7 % over 6 on C5) and 7 with a medium, exact or bounded (72 VGPRs, no spills; round 4 on the reference
+// tree chose 6: C4 5567-5573 vs 5709-5731 Mrays/s at 7, profiles/r04/knobs/waves_ab1.txt; round 6 on the SAH
+// tree, with 22 % fewer L2 requests, 7 wins: C4 8138-8149 vs 7975-7983, C4 bounded 12275-12294 vs 11489-11523,
+// profiles/r06/knobs/c4_waves.txt).
 int pass_min_waves(bool unified, int feat, bool small) {
     static int w = [] {
         const char* e = getenv("PT_MIN_WAVES");
@@ -985,13 +987,12 @@ int pass_min_waves(bool unified, int feat, bool small) {
     if (w) return w;
     if (!unified) return 8;
     // 8 without textures or media (64 VGPRs, no spills since the hit point is recomputed at use: metric +0.8 %
-    // one frame per launch, C3 +1 %); 6 with a medium even where 7 fits without spills (C4 5567-5573 vs
-    // 5709-5731 Mrays/s: more waves only thrash the 51-MB tree's cache lines; profiles/r04/knobs/waves_ab1.txt)
+    // one frame per launch, C3 +1 %); 7 with a medium (above; the bounded walk's instances exist at 6 and 7)
     static const int plain = env_int("PT_PLAIN_WAVES", 8, 5, 8);
-    static const int medium = env_int("PT_MEDIUM_WAVES", 6, 5, 8);
+    static const int medium = env_int("PT_MEDIUM_WAVES", 7, 5, 8);
     // a small launch (C1's 512x512x4 units: 128 per wave at 8 waves) is mostly its waves' first chunks and
     // tails: 7 waves (C1 33129-34058 vs 30978-31236 Mrays/s at 8, profiles/r04/knobs/c1_waves.txt)
-    return (feat & PT_FEAT_MBOUND) ? 6 : (feat & PT_FEAT_MEDIUM) ? medium : (feat & PT_FEAT_TEX) ? 7
+    return (feat & PT_FEAT_MBOUND) ? (medium >= 7 ? 7 : 6) : (feat & PT_FEAT_MEDIUM) ? medium : (feat & PT_FEAT_TEX) ? 7
                                                                                 : small ? (plain < 7 ? plain : 7) : plain;
 }
 
