@@ -990,10 +990,13 @@ int pass_min_waves(bool unified, int feat, bool small) {
     // one frame per launch, C3 +1 %); 7 with a medium (above; the bounded walk's instances exist at 6 and 7)
     static const int plain = env_int("PT_PLAIN_WAVES", 8, 5, 8);
     static const int medium = env_int("PT_MEDIUM_WAVES", 7, 5, 8);
+    // textures: 8 since round 6 (64 VGPRs with 5 cold spills, 16 B of scratch; C5 9876-9881 vs 9779-9785 Mrays/s at 7,
+    // profiles/r06/knobs/c5_waves.txt; round 4's 7 over 6 was +6.7 %)
+    static const int tex = env_int("PT_TEX_WAVES", 8, 5, 8);
     // a small launch (C1's 512x512x4 units: 128 per wave at 8 waves) is mostly its waves' first chunks and
     // tails: 7 waves (C1 33129-34058 vs 30978-31236 Mrays/s at 8, profiles/r04/knobs/c1_waves.txt)
-    return (feat & PT_FEAT_MBOUND) ? (medium >= 7 ? 7 : 6) : (feat & PT_FEAT_MEDIUM) ? medium : (feat & PT_FEAT_TEX) ? 7
-                                                                                : small ? (plain < 7 ? plain : 7) : plain;
+    return (feat & PT_FEAT_MBOUND) ? (medium >= 7 ? 7 : 6) : (feat & PT_FEAT_MEDIUM) ? medium
+                                   : small ? std::min((feat & PT_FEAT_TEX) ? tex : plain, 7) : (feat & PT_FEAT_TEX) ? tex : plain;
 }
 
 // PT_UNIFIED=0 selects pass_kernel for the default configuration (leaf size 1, uninstrumented);
